@@ -1,0 +1,270 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident soft-RSS parse+hash throughput (BASELINE.json).
+
+One "step" = one full soft-RSS pass over one batch resident in HBM: parse +
+Toeplitz hash + queue for every packet (toeplitz_dispatch,
+fs/lib/ff_dpdk_if.c:1945-2113) plus the per-queue FIFO index lists that stand
+in for process_packets' enqueue into dispatch_ring[port][q] (:1078-1094).
+
+Workload (BASELINE.json configs[1]): 64 B Eth/IPv4/UDP, 1M random 5-tuples,
+2^24 packets per GPU generated on-device, 64-byte windows + data_len;
+fs/config/config.ini knobs (nb_procs 3, soft_dispatch 1, dispatch_only_core 1).
+
+Multi-GPU: one process per GPU (torchrun), each rank classifies its own
+contiguous shard of the global packet stream — no collective on the data path
+(SURVEY.md §8(e)); gloo carries only the barrier and the max-over-ranks time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--profile udp4]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PROFILES = {"udp4_1flow": 0, "udp4": 1, "imix": 2, "vlan6_tcp": 3, "jumbo_tcp4": 4,
+            "tcp4": 5, "fuzz": 6}
+WORKLOADS = {
+    "udp4": "64B UDP/IPv4, 1M random 5-tuples (BASELINE configs[1])",
+    "imix": "IMIX 64/570/1500 7:4:1 TCP+UDP/IPv4, 1M flows (configs[2])",
+    "vlan6_tcp": "64B VLAN+IPv6+TCP, 4M flows (configs[3])",
+    "jumbo_tcp4": "9000B jumbo TCP/IPv4 header-bound, 16M flows (configs[4])",
+    "tcp4": "64B TCP/IPv4, 1M flows (hash path on every packet)",
+    "udp4_1flow": "64B UDP/IPv4 single flow (configs[0] traffic)",
+    "fuzz": "adversarial headers",
+}
+NFLOWS = {"udp4": 1 << 20, "imix": 1 << 20, "vlan6_tcp": 1 << 22, "jumbo_tcp4": 1 << 24,
+          "tcp4": 1 << 20, "udp4_1flow": 1, "fuzz": 1}
+SEED = 0x9E3779B97F4A7C15
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--profile", default="udp4", choices=sorted(PROFILES))
+    ap.add_argument("--pkts", type=int, default=1 << 24, help="packets per GPU")
+    ap.add_argument("--stride", type=int, default=64)
+    ap.add_argument("--nb-procs", type=int, default=3)
+    ap.add_argument("--nb-queues", type=int, default=None)
+    ap.add_argument("--dispatch-only-core", type=int, default=1)
+    ap.add_argument("--no-compact", action="store_true",
+                    help="parse+hash only (no per-queue lists)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target CPU-baseline duration (0 disables)")
+    ap.add_argument("--check", type=int, default=1 << 20,
+                    help="packets verified against the oracle after timing (0 = off)")
+    ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_parse_hash.json"),
+                    help="rocprofv3 PMC summary used for roofline.traffic")
+    return ap.parse_args(argv)
+
+
+# ---- distributed plumbing (gloo: control only) -----------------------------------
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+# ---- CPU baseline (oracle, rank 0 at N=1 only) ------------------------------------
+def cpu_baseline(args, nb_queues):
+    from oracle import oracle
+
+    n = 1 << 20
+    win, lens = oracle.synth(PROFILES[args.profile], n, 0, SEED, NFLOWS[args.profile],
+                             args.stride)
+    c = oracle.cfg(args.nb_procs, nb_queues, 1, args.dispatch_only_core)
+    t0 = time.perf_counter()
+    oracle.bench_dispatch(win, args.stride, lens, c, 1)
+    one = time.perf_counter() - t0
+    reps = max(1, int(args.cpu_seconds / max(one, 1e-6)))
+    t0 = time.perf_counter()
+    oracle.bench_dispatch(win, args.stride, lens, c, reps)
+    dt = time.perf_counter() - t0
+    cpu = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(reps * n / dt / 1e6, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
+        "sample": f"{reps} passes x {n} pkts of the same {args.profile} stream "
+                  f"({dt:.1f}s); bit-serial toeplitz_dispatch restatement, one call per "
+                  f"packet, gcc -O2 fs/lib flags; host CPU: {cpu}",
+    }
+
+
+def load_traffic(path: str, key: dict):
+    """Per-launch HBM bytes for the parse kernel from a committed PMC summary
+    of the same workload (profiles/pmc_parse_hash.json), else None."""
+    try:
+        d = json.loads(Path(path).read_text())
+    except (OSError, ValueError):
+        return None
+    for ent in d.get("entries", []):
+        if all(ent.get("key", {}).get(k) == v for k, v in key.items()):
+            return ent.get("hbm_bytes_per_launch")
+    return None
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    world, rank, local = dist_setup()
+    import numpy as np
+    import torch
+
+    from yastack_amd import SoftRss, abi
+    from yastack_amd.shard import shard_range
+
+    torch.cuda.set_device(local)
+    nbq = args.nb_queues or args.nb_procs
+    eng = SoftRss(nb_procs=args.nb_procs, nb_queues=nbq, soft_dispatch=1,
+                  dispatch_only_core=args.dispatch_only_core, device=local, max_burst=0)
+    n = args.pkts
+    first = rank * n                      # weak scaling: rank r owns shard r of the stream
+    prof = PROFILES[args.profile]
+    win, lens = eng.synth(prof, n, first, SEED, NFLOWS[args.profile], args.stride)
+    out = eng.alloc_out(n, win.device, want_hash=True, compact=not args.no_compact)
+    torch.cuda.synchronize()
+
+    def step():
+        eng.dispatch_dev(win, lens, args.stride, n, out=out, compact=not args.no_compact)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng.timing_enable(1 << abi.K_PARSE_HASH)   # events bracket the dominant kernel only
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    elapsed = max_over_ranks(t1 - t0, world)
+    k_ms, k_cnt = eng.timing_read(abi.K_PARSE_HASH)
+    eng.timing_enable(0)
+    k_avg_s = max_over_ranks(k_ms / max(k_cnt, 1) / 1e3, world)
+
+    total_pkts = sum_over_ranks(float(n * args.steps), world)
+    value = total_pkts / elapsed / 1e6
+    # algorithmic bytes per packet for the parse kernel: header window read
+    # (min(stride, 64) — the kernel stages 64 B), data_len read (2), hash (4) and
+    # queue (2) written = 72 B at 64-B windows.
+    bpp = min(args.stride, 64) + 2 + 4 + 2
+    achieved = bpp * n / k_avg_s / 1e9
+    key = {"profile": args.profile, "pkts": n, "stride": args.stride,
+           "compact": not args.no_compact}
+    traffic = load_traffic(args.pmc, key)
+
+    check = None
+    if args.check:
+        from oracle import oracle
+
+        m = min(args.check, n)
+        c = oracle.cfg(args.nb_procs, nbq, 1, args.dispatch_only_core)
+        w_h = win[: m * args.stride].cpu().numpy()
+        l_h = lens[:m].cpu().numpy().view(np.uint16)
+        q_ref, h_ref = oracle.dispatch_windows(w_h, args.stride, l_h, c)
+        ok = bool(np.array_equal(out.q[:m].cpu().numpy(), q_ref) and
+                  np.array_equal(out.hash[:m].cpu().numpy().view(np.uint32), h_ref))
+        if not args.no_compact:
+            q_all = out.q[:n].cpu().numpy()
+            qi_ref, qs_ref = oracle.process_burst(q_all, nbq)
+            ok = ok and bool(np.array_equal(out.qstart.cpu().numpy().view(np.uint32), qs_ref) and
+                             np.array_equal(out.qidx[:n].cpu().numpy().view(np.uint32), qi_ref))
+        check = {"pkts_checked": m, "bit_exact": ok}
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args, nbq)
+
+    if rank == 0:
+        line = {
+            "metric": "Mpkt/s device-resident soft-RSS parse+hash, 64B pkts, 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "Mpkt/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (on-device counter-based generator, include/yrss_synth.h)",
+            "config": {
+                "workload": WORKLOADS[args.profile],
+                "pkts_per_gpu": n, "logical_burst": 1024, "win_stride": args.stride,
+                "nb_procs": args.nb_procs, "nb_queues": nbq, "soft_dispatch": 1,
+                "dispatch_only_core": args.dispatch_only_core,
+                "per_queue_lists": not args.no_compact,
+                "parallelism": f"shard{world}",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": "yrss_parse_hash", "bytes_per_pkt": bpp,
+                "kernel_avg_us": round(k_avg_s * 1e6, 2),
+            },
+            "cpu_baseline": cpu,
+            "check": check,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

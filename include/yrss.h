@@ -1,0 +1,206 @@
+/*
+ * yrss.h — C ABI of the MI355X software-RSS engine (parse + Toeplitz hash +
+ * per-queue dispatch) that replaces yastack / F-Stack's soft-dispatch path.
+ *
+ * Reference path being replaced (all paths relative to the yastack tree):
+ *   fs/lib/ff_api.h:167-174        dispatch_func_t, ff_regist_packet_dispatcher,
+ *                                  toeplitz_dispatch prototypes
+ *   fs/lib/ff_dpdk_if.c:1881-1902  toeplitz_hash (bit-serial Toeplitz)
+ *   fs/lib/ff_dpdk_if.c:1945-2113  toeplitz_dispatch (L2/L3/L4 parse + queue)
+ *   fs/lib/ff_dpdk_if.c:1058-1094  process_packets dispatcher block (drop if
+ *                                  ret<0 || ret>=nb_queues, else enqueue to
+ *                                  dispatch_ring[port][ret])
+ *   fs/lib/ff_dpdk_if.c:1653-1683  main_loop_vm_3 RX burst → per-packet loop
+ *
+ * The reference calls its dispatcher once per packet on the CPU.  This ABI is
+ * burst-shaped instead: the hook sits between rte_eth_rx_burst
+ * (ff_dpdk_if.c:1655) and the per-packet loop (:1674), classifies a whole
+ * batch on the GPU, and returns per-packet {queue, hash} plus per-queue FIFO
+ * index lists (the device-side analogue of dispatch_ring[port][q]).
+ *
+ * Everything here is plain C: pointers, sizes, ints.  No HIP or torch types
+ * appear in signatures; device pointers are `void *`/typed pointers to device
+ * memory and HIP streams are passed as `void *` (hipStream_t, NULL = default).
+ *
+ * Errors: every int-returning call returns 0 on success or a negative errno
+ * (-EINVAL bad argument, -ENOMEM allocation failure, -ENODEV no usable GPU,
+ * -EIO HIP runtime failure).  This mirrors the reference's only error channel
+ * (the sign of the dispatcher's return, ff_api.h:160-163) — there is no errno.
+ */
+#ifndef YRSS_H
+#define YRSS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YRSS_VERSION_STRING "yrss 0.1.0 (gfx950)"
+
+/* ---- constants mirrored from the reference -------------------------------- */
+
+/* Toeplitz key length used by the reference: sizeof(default_rsskey_40bytes),
+ * fs/lib/ff_dpdk_if.c:113-119. */
+#define YRSS_RSS_KEY_LEN 40
+
+/* Default queue returned for every packet the reference does not hash
+ * (`uint16_t default_Q = 2`, ff_dpdk_if.c:1948). */
+#define YRSS_DEFAULT_Q 2
+
+/* Queue written for a hashed TCP packet whose L4 ports lie beyond the bytes
+ * the caller staged in its header window (only possible when win_stride < 78
+ * and data_len > win_stride).  Never produced by yrss_dispatch_burst /
+ * yrss_dispatch_frames, which always stage enough bytes.  Such packets land
+ * in the drop bucket, like any ret outside [0, nb_queues). */
+#define YRSS_Q_TRUNCATED (-2)
+
+/* Widest header window the parse ever needs: with IHL=15 the TCP ports sit at
+ * bytes 74..77 (14 + 60 + 4).  A window stride >= 80 never truncates. */
+#define YRSS_WIN_FULL 80
+/* Minimum window stride: one 64-byte coalesced header block per packet. */
+#define YRSS_WIN_MIN 64
+
+/* Largest supported values (queues are buckets of the compaction; q is int16). */
+#define YRSS_MAX_QUEUES 256
+#define YRSS_MAX_PROCS 4096
+
+/* struct rte_mbuf field offsets for the in-tree DPDK 18.02 (x86_64), measured
+ * from dpdk/lib/librte_mbuf/rte_mbuf.h:412-560.  The burst API reads
+ * buf_addr/data_off/data_len and may write hash.rss; callers on another DPDK
+ * version override them in yrss_config.mbuf. */
+#define YRSS_MBUF_OFF_BUF_ADDR 0
+#define YRSS_MBUF_OFF_DATA_OFF 16
+#define YRSS_MBUF_OFF_DATA_LEN 40
+#define YRSS_MBUF_OFF_HASH_RSS 44
+
+struct yrss_mbuf_layout {
+    uint16_t off_buf_addr;   /* void *buf_addr                         */
+    uint16_t off_data_off;   /* uint16_t data_off                      */
+    uint16_t off_data_len;   /* uint16_t data_len (first segment only) */
+    uint16_t off_hash_rss;   /* uint32_t hash.rss                      */
+};
+
+/* ---- configuration --------------------------------------------------------- */
+
+/* The knobs toeplitz_dispatch / process_packets read:
+ *   rss_key            default_rsskey_40bytes           ff_dpdk_if.c:113-119
+ *   nb_procs           ff_global_cfg.dpdk.nb_procs      ff_config.c:133 (popcount lcore_mask)
+ *   soft_dispatch      ff_global_cfg.dpdk.soft_dispatch ff_config.c:440-441
+ *   dispatch_only_core ff_global_cfg.system.dispatch_only_core  ff_config.c:450-451
+ *   nb_queues          qconf->nb_queue_list[port]       ff_dpdk_if.c:1063, :420
+ */
+struct yrss_config {
+    uint8_t  rss_key[YRSS_RSS_KEY_LEN];
+    uint32_t rss_key_len;          /* 4..40; the reference always uses 40   */
+    int32_t  nb_procs;             /* 1..YRSS_MAX_PROCS                     */
+    uint16_t nb_queues;            /* 1..YRSS_MAX_QUEUES (drop if q>=this)  */
+    uint8_t  soft_dispatch;        /* 0/1                                   */
+    uint8_t  dispatch_only_core;   /* 0/1; with soft_dispatch needs nb_procs>=2 */
+    int32_t  device;               /* HIP device ordinal for yrss_init      */
+    uint32_t max_burst;            /* host-burst staging capacity (packets) */
+    struct yrss_mbuf_layout mbuf;  /* rte_mbuf offsets for the burst API    */
+};
+
+/* Fill cfg with the reference defaults: the Mellanox key, the shipped
+ * fs/config/config.ini (lcore_mask=7 → nb_procs=3, soft_dispatch=1,
+ * dispatch_only_core=1), nb_queues=nb_procs, device 0, DPDK 18.02 mbuf. */
+void yrss_config_default(struct yrss_config *cfg);
+
+/* Validate without touching the GPU.  Rejects what the reference would divide
+ * by zero on (dispatch_only_core && soft_dispatch && nb_procs < 2,
+ * ff_dpdk_if.c:2031-2032) and out-of-range sizes.  0 or -EINVAL. */
+int yrss_config_validate(const struct yrss_config *cfg);
+
+/* ---- context ------------------------------------------------------------------ */
+
+typedef struct yrss_ctx yrss_ctx;
+
+/* Create a context bound to cfg->device: uploads the key schedule, sizes the
+ * compaction workspace, allocates pinned staging for max_burst packets.
+ * One context per host thread (the reference's dispatcher is single-threaded,
+ * ff_dpdk_if.c:1653). */
+int  yrss_init(const struct yrss_config *cfg, yrss_ctx **out);
+void yrss_fini(yrss_ctx *ctx);
+
+/* ---- device-resident dispatch (the metric path) ------------------------------ */
+
+/* Classify n packets whose header windows already sit in HBM.
+ *   d_win      window i at d_win + i*win_stride holds bytes
+ *              [0, min(len_i, win_stride)) of packet i's first segment;
+ *              16-byte aligned, win_stride % 16 == 0, win_stride >= 64.
+ *   d_len      n x uint16 data_len (rte_pktmbuf_data_len, ff_dpdk_if.c:1076)
+ *   d_q        n x int16 queue = toeplitz_dispatch's return
+ *   d_hash     n x uint32 Toeplitz hash (0 where the reference does not hash);
+ *              may be NULL
+ *   d_qidx     n x uint32 packet indices grouped by bucket, FIFO inside each
+ *              bucket; may be NULL (then d_qstart is ignored)
+ *   d_qstart   nb_queues+2 x uint32: bucket b in [0,nb_queues) holds the
+ *              packets dispatched to queue b; bucket nb_queues holds the
+ *              packets process_packets frees (ret<0 || ret>=nb_queues,
+ *              ff_dpdk_if.c:1080-1083).  Bucket b = d_qidx[d_qstart[b] ..
+ *              d_qstart[b+1]).  d_qstart[nb_queues+1] == n.
+ *   stream     hipStream_t (NULL = legacy default stream)
+ * Asynchronous: returns after enqueueing the kernels. */
+int yrss_dispatch_dev(yrss_ctx *ctx, const uint8_t *d_win, uint32_t win_stride,
+                      const uint16_t *d_len, uint32_t n, int16_t *d_q,
+                      uint32_t *d_hash, uint32_t *d_qidx, uint32_t *d_qstart,
+                      void *stream);
+
+/* ---- host-resident dispatch (the drop-in burst hook) ------------------------ */
+
+/* Classify a burst of DPDK mbufs straight off rte_eth_rx_burst.
+ *   mbufs      n x `struct rte_mbuf *` (read per cfg->mbuf offsets)
+ *   out_q      n x int16 host array (required)
+ *   out_hash   n x uint32 host array or NULL
+ *   out_qidx / out_qstart  host arrays as in yrss_dispatch_dev, or NULL
+ *   flags      YRSS_F_WRITE_RSS: also store each hash into mbuf hash.rss
+ * Gathers min(data_len, 64 or 80) header bytes into pinned memory, copies to
+ * the GPU, runs the same kernels, copies back.  Synchronous. */
+#define YRSS_F_WRITE_RSS 0x1u
+int yrss_dispatch_burst(yrss_ctx *ctx, void *const *mbufs, uint32_t n,
+                        int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx,
+                        uint32_t *out_qstart, uint32_t flags);
+
+/* Same, for frames given as (data pointer, data_len) pairs. */
+int yrss_dispatch_frames(yrss_ctx *ctx, const uint8_t *const *data,
+                         const uint16_t *len, uint32_t n, int16_t *out_q,
+                         uint32_t *out_hash, uint32_t *out_qidx,
+                         uint32_t *out_qstart);
+
+/* ---- synthetic traffic (bench / parity inputs; see yrss_synth.h) ------------- */
+
+struct yrss_synth_params;
+/* Write header windows + data_len of packets [first, first+n) of a synthetic
+ * stream directly into HBM.  Bit-identical to yrss_synth_window() on the host. */
+int yrss_synth_dev(yrss_ctx *ctx, const struct yrss_synth_params *p,
+                   uint64_t first, uint32_t n, uint8_t *d_win,
+                   uint32_t win_stride, uint16_t *d_len, void *stream);
+
+/* ---- timing hook (bench) ------------------------------------------------------- */
+
+/* kernel_mask bit k (YRSS_K_*) brackets every launch of kernel k by
+ * yrss_dispatch_dev with hipEvents on the launch stream (0 disables; enabling
+ * resets the totals).  yrss_timing_read synchronises the pending events and
+ * returns the summed milliseconds and launch count for one kernel. */
+#define YRSS_K_PARSE_HASH 0
+#define YRSS_K_SCAN       1
+#define YRSS_K_SCATTER    2
+#define YRSS_K_COUNT      3
+int yrss_timing_enable(yrss_ctx *ctx, int kernel_mask);
+int yrss_timing_read(yrss_ctx *ctx, int kernel, double *total_ms,
+                     uint32_t *launches);
+
+/* ---- introspection --------------------------------------------------------------- */
+
+const char *yrss_version(void);
+/* Kernel-name string as it appears in rocprof traces, for kernel id k. */
+const char *yrss_kernel_name(int kernel);
+/* Number of workgroups the parse+hash kernel will use for n packets. */
+uint32_t yrss_grid_for(yrss_ctx *ctx, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YRSS_H */

@@ -1,0 +1,40 @@
+#!/bin/sh
+# ORACLE — TEST INFRASTRUCTURE ONLY.
+#
+# Compile the reference's own Toeplitz engine from its source, where it lies,
+# into oracle/_ref/libref_thash.so.  Two pieces of fs/lib/ff_dpdk_if.c need
+# nothing beyond the C library and are compiled verbatim:
+#   default_rsskey_40bytes   ff_dpdk_if.c:113-119
+#   toeplitz_hash            ff_dpdk_if.c:1881-1902
+# They are streamed into gcc on stdin (no source file is written anywhere), and
+# two extern wrappers expose them.  toeplitz_dispatch itself is NOT built: it
+# needs DPDK headers that require DPDK's generated rte_build_config.h, which
+# the image lacks, so it is unbuildable here.
+#
+# Output: oracle/_ref/libref_thash.so (git-ignored, travels to the GPU box).
+set -eu
+HERE=$(cd "$(dirname "$0")" && pwd)
+REF=${YRSS_REFERENCE:-/root/reference}
+SRC="$REF/fs/lib/ff_dpdk_if.c"
+if [ ! -f "$SRC" ]; then
+    echo "build_ref.sh: $SRC not present; oracle/_ref not built" >&2
+    exit 0
+fi
+mkdir -p "$HERE/_ref"
+{
+    printf '#include <stdint.h>\n#include <sys/types.h>\n'
+    printf '#line 1 "%s"\n' "$SRC"
+    awk '/^static uint8_t default_rsskey_40bytes/ {f = 1} f {print} f && /^};/ {exit}' "$SRC"
+    awk 'prev ~ /^static uint32_t[ \t]*$/ && /^toeplitz_hash\(/ {print prev; f = 1}
+         f {print}
+         f && /^}/ {exit}
+         {prev = $0}' "$SRC"
+    cat <<'EOF'
+uint32_t ref_toeplitz_hash(unsigned keylen, const uint8_t *key,
+                           unsigned datalen, const uint8_t *data)
+{ return toeplitz_hash(keylen, key, datalen, data); }
+const uint8_t *ref_default_rsskey(void) { return default_rsskey_40bytes; }
+EOF
+} | ${CC:-gcc} -O2 -frename-registers -funswitch-loops -fweb -fPIC -shared -x c - \
+      -o "$HERE/_ref/libref_thash.so"
+echo "build_ref.sh: built $HERE/_ref/libref_thash.so"

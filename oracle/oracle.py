@@ -1,0 +1,149 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+ctypes loader for oracle/liboracle.so (the C restatement in yrss_oracle.c)
+and, when present, oracle/_ref/libref_thash.so (the reference's own
+toeplitz_hash compiled by build_ref.sh).  Imported only by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB = HERE / "liboracle.so"
+REF_LIB = HERE / "_ref" / "libref_thash.so"
+
+MLX_KEY = bytes.fromhex(
+    "d181c62cf7f4db5b1983a2fc943e1adbd9389e6bd1039c2ca74499ad593d56d9f3253c062adc1ffc")
+
+
+class OracleCfg(ctypes.Structure):
+    _fields_ = [
+        ("key", ctypes.c_uint8 * 40),
+        ("keylen", ctypes.c_uint32),
+        ("nb_procs", ctypes.c_int32),
+        ("nb_queues", ctypes.c_uint16),
+        ("soft_dispatch", ctypes.c_uint8),
+        ("dispatch_only_core", ctypes.c_uint8),
+    ]
+
+
+class SynthParams(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("profile", ctypes.c_uint32),
+                ("nflows", ctypes.c_uint32)]
+
+
+_lib = None
+_ref = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", str(HERE), "all"], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB.exists():
+            build()
+        L = ctypes.CDLL(str(LIB))
+        vp, u32 = ctypes.c_void_p, ctypes.c_uint32
+        L.oracle_toeplitz_hash.restype = u32
+        L.oracle_toeplitz_hash.argtypes = [ctypes.c_uint, ctypes.c_char_p, ctypes.c_uint,
+                                           ctypes.c_char_p]
+        L.oracle_toeplitz_dispatch.restype = ctypes.c_int
+        L.oracle_toeplitz_dispatch.argtypes = [ctypes.c_char_p, ctypes.c_uint16,
+                                               ctypes.POINTER(OracleCfg),
+                                               ctypes.POINTER(ctypes.c_uint32)]
+        L.oracle_dispatch_windows.restype = None
+        L.oracle_dispatch_windows.argtypes = [vp, u32, vp, u32, ctypes.POINTER(OracleCfg), vp,
+                                              vp, ctypes.c_int]
+        L.oracle_process_burst.restype = None
+        L.oracle_process_burst.argtypes = [vp, u32, ctypes.c_uint16, vp, vp]
+        L.oracle_ff_rss_check.restype = ctypes.c_int
+        L.oracle_ff_rss_check.argtypes = [ctypes.POINTER(OracleCfg), ctypes.c_uint16,
+                                          ctypes.c_uint16, ctypes.c_uint16, u32, u32,
+                                          ctypes.c_uint16, ctypes.c_uint16]
+        L.oracle_synth.restype = None
+        L.oracle_synth.argtypes = [ctypes.POINTER(SynthParams), ctypes.c_uint64, u32, vp, u32, vp]
+        L.oracle_bench_dispatch.restype = ctypes.c_uint64
+        L.oracle_bench_dispatch.argtypes = [vp, u32, vp, u32, ctypes.POINTER(OracleCfg), u32,
+                                            ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def ref():
+    """The reference's compiled toeplitz_hash, or None if oracle/_ref is absent."""
+    global _ref
+    if _ref is None and REF_LIB.exists():
+        R = ctypes.CDLL(str(REF_LIB))
+        R.ref_toeplitz_hash.restype = ctypes.c_uint32
+        R.ref_toeplitz_hash.argtypes = [ctypes.c_uint, ctypes.c_char_p, ctypes.c_uint,
+                                        ctypes.c_char_p]
+        R.ref_default_rsskey.restype = ctypes.POINTER(ctypes.c_uint8)
+        _ref = R
+    return _ref
+
+
+def cfg(nb_procs=3, nb_queues=None, soft_dispatch=1, dispatch_only_core=1,
+        key: bytes = MLX_KEY) -> OracleCfg:
+    c = OracleCfg()
+    ctypes.memmove(c.key, key, len(key))
+    c.keylen = len(key)
+    c.nb_procs = nb_procs
+    c.nb_queues = nb_procs if nb_queues is None else nb_queues
+    c.soft_dispatch = soft_dispatch
+    c.dispatch_only_core = dispatch_only_core
+    return c
+
+
+def toeplitz_hash(data: bytes, key: bytes = MLX_KEY) -> int:
+    return lib().oracle_toeplitz_hash(len(key), key, len(data), data)
+
+
+def toeplitz_dispatch(frame: bytes, length: int, c: OracleCfg) -> tuple[int, int]:
+    h = ctypes.c_uint32()
+    buf = bytes(frame) + bytes(max(0, 80 - len(frame)))
+    q = lib().oracle_toeplitz_dispatch(buf, length, ctypes.byref(c), ctypes.byref(h))
+    return q, h.value
+
+
+def dispatch_windows(win: np.ndarray, stride: int, lens: np.ndarray, c: OracleCfg,
+                     fast: bool = True):
+    n = int(lens.size)
+    win = np.ascontiguousarray(win, dtype=np.uint8)
+    lens = np.ascontiguousarray(lens).view(np.uint16)
+    q = np.empty(max(n, 1), np.int16)
+    h = np.empty(max(n, 1), np.uint32)
+    lib().oracle_dispatch_windows(win.ctypes.data, stride, lens.ctypes.data, n, ctypes.byref(c),
+                                  q.ctypes.data, h.ctypes.data, 1 if fast else 0)
+    return q[:n], h[:n]
+
+
+def process_burst(q: np.ndarray, nb_queues: int):
+    n = int(q.size)
+    q = np.ascontiguousarray(q, dtype=np.int16)
+    qi = np.empty(max(n, 1), np.uint32)
+    qs = np.empty(nb_queues + 2, np.uint32)
+    lib().oracle_process_burst(q.ctypes.data, n, nb_queues, qi.ctypes.data, qs.ctypes.data)
+    return qi[:n], qs
+
+
+def synth(profile: int, n: int, first: int = 0, seed: int = 0x9E3779B97F4A7C15,
+          nflows: int = 1 << 20, stride: int = 64):
+    win = np.empty(max(n, 1) * stride, np.uint8)
+    lens = np.empty(max(n, 1), np.uint16)
+    p = SynthParams(seed & 0xFFFFFFFFFFFFFFFF, profile, nflows)
+    lib().oracle_synth(ctypes.byref(p), first, n, win.ctypes.data, stride, lens.ctypes.data)
+    return win[:n * stride], lens[:n]
+
+
+def bench_dispatch(win, stride, lens, c: OracleCfg, reps: int, fast: bool = False) -> int:
+    lens = np.ascontiguousarray(lens).view(np.uint16)
+    return lib().oracle_bench_dispatch(win.ctypes.data, stride, lens.ctypes.data, int(lens.size),
+                                       ctypes.byref(c), reps, 1 if fast else 0)

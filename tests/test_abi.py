@@ -1,0 +1,97 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+function include/yrss.h declares, validates configs like the reference would
+fail them, and the Python constants agree with the header."""
+import ctypes
+import errno
+import re
+import subprocess
+
+import pytest
+
+from yastack_amd import abi
+
+
+def test_library_exports_every_header_function():
+    lib = abi.load()
+    names = abi.header_functions()
+    assert len(names) >= 13
+    out = subprocess.run(["nm", "-D", "--defined-only", str(abi.LIB_PATH)],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (yrss_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    for n in names:
+        assert getattr(lib, n) is not None
+
+
+def test_library_is_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", str(abi.LIB_PATH)],
+                         capture_output=True, text=True).stdout
+    # offload bundle carries the gfx950 code object
+    data = abi.LIB_PATH.read_bytes()
+    assert b"gfx950" in data
+
+
+def test_header_constants_match_python():
+    text = abi.HEADER_PATH.read_text()
+    consts = dict(re.findall(r"#define (YRSS_\w+)\s+\(?(-?[0-9x]+)u?\)?", text))
+    assert int(consts["YRSS_RSS_KEY_LEN"]) == abi.RSS_KEY_LEN
+    assert int(consts["YRSS_DEFAULT_Q"]) == abi.DEFAULT_Q
+    assert int(consts["YRSS_Q_TRUNCATED"]) == abi.Q_TRUNCATED
+    assert int(consts["YRSS_WIN_FULL"]) == abi.WIN_FULL
+    assert int(consts["YRSS_WIN_MIN"]) == abi.WIN_MIN
+    assert int(consts["YRSS_MBUF_OFF_DATA_LEN"]) == abi.MBUF_OFF_DATA_LEN
+    assert int(consts["YRSS_MBUF_OFF_HASH_RSS"]) == abi.MBUF_OFF_HASH_RSS
+    assert ctypes.sizeof(abi.Config) == 40 + 4 + 4 + 2 + 1 + 1 + 4 + 4 + 8
+
+
+def test_default_config_is_reference_defaults():
+    from oracle.oracle import MLX_KEY
+
+    cfg = abi.default_config()
+    assert bytes(cfg.rss_key) == MLX_KEY          # ff_dpdk_if.c:113-119
+    assert cfg.rss_key_len == 40
+    assert (cfg.nb_procs, cfg.soft_dispatch, cfg.dispatch_only_core) == (3, 1, 1)  # config.ini
+    assert cfg.mbuf.off_data_len == 40 and cfg.mbuf.off_data_off == 16
+
+
+@pytest.mark.parametrize("field,value,ok", [
+    ("nb_procs", 0, False), ("nb_procs", 1, False),      # doc=1 → hash % 0 (ff_dpdk_if.c:2032)
+    ("nb_procs", 2, True), ("nb_procs", 4096, True), ("nb_procs", 4097, False),
+    ("nb_queues", 0, False), ("nb_queues", 256, True), ("nb_queues", 257, False),
+    ("rss_key_len", 3, False), ("rss_key_len", 41, False), ("rss_key_len", 4, True),
+    ("soft_dispatch", 2, False), ("device", -1, False),
+])
+def test_config_validate(field, value, ok):
+    cfg = abi.default_config()
+    setattr(cfg, field, value)
+    rc = abi.load().yrss_config_validate(ctypes.byref(cfg))
+    assert (rc == 0) == ok
+    if not ok:
+        assert rc == -errno.EINVAL
+
+
+def test_nb_procs_one_ok_without_dispatch_only_core():
+    cfg = abi.default_config()
+    cfg.nb_procs = 1
+    cfg.dispatch_only_core = 0
+    assert abi.load().yrss_config_validate(ctypes.byref(cfg)) == 0
+
+
+def test_init_without_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    cfg = abi.default_config()
+    ctx = ctypes.c_void_p()
+    rc = abi.load().yrss_init(ctypes.byref(cfg), ctypes.byref(ctx))
+    assert rc < 0 and not ctx.value
+
+
+def test_missing_library_raises(monkeypatch, tmp_path):
+    monkeypatch.setattr(abi, "_lib", None)
+    monkeypatch.setenv("YRSS_LIB", str(tmp_path / "nope.so"))
+    with pytest.raises(abi.YrssLibraryError):
+        abi.load()
+    monkeypatch.delenv("YRSS_LIB")

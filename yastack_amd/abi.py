@@ -1,0 +1,152 @@
+"""ctypes binding of the C ABI in include/yrss.h.
+
+The shared library ``yastack_amd/_lib/libyrss.so`` is built in-tree by
+``__graft_entry__.build()`` (hipcc --offload-arch=gfx950).  There is no
+fallback: if the library is missing, every entry point raises
+:class:`YrssLibraryError` — the product path never degrades to a CPU
+implementation.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno
+import os
+import re
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+LIB_PATH = PKG_DIR / "_lib" / "libyrss.so"
+HEADER_PATH = REPO_DIR / "include" / "yrss.h"
+
+RSS_KEY_LEN = 40
+DEFAULT_Q = 2
+Q_TRUNCATED = -2
+WIN_MIN = 64
+WIN_FULL = 80
+MAX_QUEUES = 256
+MAX_PROCS = 4096
+F_WRITE_RSS = 0x1
+
+K_PARSE_HASH, K_SCAN, K_SCATTER = 0, 1, 2
+
+# struct rte_mbuf offsets of DPDK 18.02 (dpdk/lib/librte_mbuf/rte_mbuf.h:412-560)
+MBUF_OFF_BUF_ADDR = 0
+MBUF_OFF_DATA_OFF = 16
+MBUF_OFF_DATA_LEN = 40
+MBUF_OFF_HASH_RSS = 44
+
+# synthetic profiles (include/yrss_synth.h)
+SYN_UDP4_1FLOW, SYN_UDP4, SYN_IMIX, SYN_VLAN6_TCP, SYN_JUMBO_TCP4, SYN_TCP4, SYN_FUZZ = range(7)
+SYN_NAMES = {
+    SYN_UDP4_1FLOW: "udp4_1flow", SYN_UDP4: "udp4", SYN_IMIX: "imix",
+    SYN_VLAN6_TCP: "vlan6_tcp", SYN_JUMBO_TCP4: "jumbo_tcp4", SYN_TCP4: "tcp4",
+    SYN_FUZZ: "fuzz",
+}
+
+
+class YrssLibraryError(RuntimeError):
+    """The HIP library is missing or failed to load (no silent fallback)."""
+
+
+class YrssError(OSError):
+    """A C-ABI call returned a negative errno."""
+
+
+class MbufLayout(ctypes.Structure):
+    _fields_ = [
+        ("off_buf_addr", ctypes.c_uint16),
+        ("off_data_off", ctypes.c_uint16),
+        ("off_data_len", ctypes.c_uint16),
+        ("off_hash_rss", ctypes.c_uint16),
+    ]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("rss_key", ctypes.c_uint8 * RSS_KEY_LEN),
+        ("rss_key_len", ctypes.c_uint32),
+        ("nb_procs", ctypes.c_int32),
+        ("nb_queues", ctypes.c_uint16),
+        ("soft_dispatch", ctypes.c_uint8),
+        ("dispatch_only_core", ctypes.c_uint8),
+        ("device", ctypes.c_int32),
+        ("max_burst", ctypes.c_uint32),
+        ("mbuf", MbufLayout),
+    ]
+
+
+class SynthParams(ctypes.Structure):
+    _fields_ = [
+        ("seed", ctypes.c_uint64),
+        ("profile", ctypes.c_uint32),
+        ("nflows", ctypes.c_uint32),
+    ]
+
+
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_PROTOS = {
+    "yrss_version": (ctypes.c_char_p, []),
+    "yrss_kernel_name": (ctypes.c_char_p, [ctypes.c_int]),
+    "yrss_config_default": (None, [ctypes.POINTER(Config)]),
+    "yrss_config_validate": (ctypes.c_int, [ctypes.POINTER(Config)]),
+    "yrss_init": (ctypes.c_int, [ctypes.POINTER(Config), ctypes.POINTER(_vp)]),
+    "yrss_fini": (None, [_vp]),
+    "yrss_dispatch_dev": (ctypes.c_int, [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "yrss_dispatch_burst": (ctypes.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]),
+    "yrss_dispatch_frames": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp]),
+    "yrss_synth_dev": (ctypes.c_int, [_vp, ctypes.POINTER(SynthParams), ctypes.c_uint64, _u32,
+                                      _vp, _u32, _vp, _vp]),
+    "yrss_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "yrss_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(_u32)]),
+    "yrss_grid_for": (_u32, [_vp, _u32]),
+}
+
+_lib = None
+
+
+def header_functions(path: Path = HEADER_PATH) -> list[str]:
+    """Names of every function declared in include/yrss.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"#define[^\n]*", "", text)
+    names = re.findall(r"\b(yrss_[a-z0-9_]+)\s*\(", text)
+    return sorted(set(names))
+
+
+def load() -> ctypes.CDLL:
+    """Load libyrss.so (once).  Raises YrssLibraryError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = Path(os.environ.get("YRSS_LIB", LIB_PATH))
+    if not path.exists():
+        raise YrssLibraryError(
+            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    try:
+        lib = ctypes.CDLL(str(path))
+    except OSError as e:  # pragma: no cover - environment specific
+        raise YrssLibraryError(f"cannot load {path}: {e}") from e
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc < 0:
+        raise YrssError(-rc, f"{what}: {os.strerror(-rc)} (errno {-rc})")
+
+
+def default_config() -> Config:
+    cfg = Config()
+    load().yrss_config_default(ctypes.byref(cfg))
+    return cfg
+
+
+__all__ = [n for n in dir() if not n.startswith("_")] + ["errno"]

@@ -1,0 +1,952 @@
+// yrss.hip — MI355X (gfx950) software-RSS engine: HIP kernels + the C ABI
+// declared in include/yrss.h.
+//
+// Replaces, for a whole batch at once, the per-packet CPU path of yastack's
+// F-Stack layer:
+//   toeplitz_dispatch   fs/lib/ff_dpdk_if.c:1945-2113  (parse + queue)
+//   toeplitz_hash       fs/lib/ff_dpdk_if.c:1881-1902  (bit-serial Toeplitz)
+//   process_packets     fs/lib/ff_dpdk_if.c:1078-1094  (drop / enqueue to
+//                                                        dispatch_ring[q])
+//
+// Three kernels per batch, all integer/byte work (no MFMA), HBM-bound:
+//   1. yrss_parse_hash  one lane per packet.  A wave owns a contiguous segment
+//      of packets and walks it in 64-packet tiles: four coalesced 16-byte
+//      loads per lane bring the tile's 64-byte header windows in (1 KiB per
+//      wave-instruction), they are staged through a wave-private 4 KiB LDS
+//      tile in an XOR-swizzled packet-major layout, and each lane then reads
+//      its own packet's fields back conflict-free.  The Toeplitz hash is 12
+//      byte-table lookups in LDS (tables built per workgroup from the key
+//      schedule); hash % nb_procs is a Lemire fastmod.  Writes q (int16) and
+//      hash (u32); counts packets per bucket per wave segment with
+//      ballot/readlane (one LDS update per distinct bucket per tile).
+//   2. yrss_seg_scan    per bucket, exclusive scan of the segment counts.
+//   3. yrss_scatter     each wave re-reads its segment's q (2 B/pkt) and writes
+//      packet indices into the per-bucket lists with ballot ranks, in packet
+//      order — the stable compaction that stands in for the FIFO
+//      rte_ring_enqueue into dispatch_ring[port][q] (ff_dpdk_if.c:1087-1093).
+#include <hip/hip_runtime.h>
+
+#include <errno.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "yrss.h"
+#include "yrss_synth.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kTile = 64;              // packets per wave-tile (one per lane)
+constexpr int kParseBlock = 256;       // 4 waves per workgroup
+constexpr int kParseWaves = kParseBlock / kWave;
+constexpr int kScatterRound = 8;       // packets per lane per scatter round
+constexpr int kTblBytes = 12 * 256 * 4;
+constexpr int kStageBytes = kTile * 64; // 4 KiB per wave
+
+// Everything yrss_parse_hash needs, passed by value (kernarg segment).
+struct ParseParams {
+    const uint8_t *win;
+    const uint16_t *len;
+    int16_t *q;
+    uint32_t *hash;       // may be null
+    uint32_t *seg_cnt;    // [segments][nb] or null (no compaction)
+    uint32_t n;
+    uint32_t stride;
+    uint32_t seg;         // packets per wave segment, multiple of kTile
+    uint32_t nq;          // nb_queues
+    uint32_t nb;          // buckets = nq + 1 (last = drop)
+    uint32_t mod_d;       // divisor: nb_procs or nb_procs-1
+    uint32_t q_off;       // 0 or 1 (dispatch_only_core)
+    uint32_t pad_;
+    uint64_t mod_m;       // Lemire fastmod constant for mod_d
+    uint32_t kwin[96];    // key window at every tuple bit position
+};
+
+struct ScatterParams {
+    const int16_t *q;
+    const uint32_t *seg_off;   // [segments][nb] exclusive per-bucket scan
+    const uint32_t *totals;    // [nb]
+    uint32_t *qidx;
+    uint32_t *qstart;          // [nb + 1]
+    uint32_t n;
+    uint32_t seg;
+    uint32_t nq;
+    uint32_t nb;
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t rank_below(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t bucket_of(int qv, uint32_t nq)
+{
+    return (qv >= 0 && (uint32_t)qv < nq) ? (uint32_t)qv : nq;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 1: parse + Toeplitz hash + queue, one lane per packet.
+// ---------------------------------------------------------------------------
+template <bool kCount>
+__global__ __launch_bounds__(kParseBlock) void yrss_parse_hash(ParseParams P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t *tbl = reinterpret_cast<uint32_t *>(smem);
+    const uint32_t wave = threadIdx.x / kWave;
+    const uint32_t lane = lane_id();
+    uint4 *stage = reinterpret_cast<uint4 *>(smem + kTblBytes + wave * kStageBytes);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + kTblBytes + kParseWaves * kStageBytes) +
+                    wave * P.nb;
+
+    // Byte tables: tbl[j*256+v] = XOR of key windows at bits 8j+b, v's bit b set.
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        for (uint32_t v = threadIdx.x; v < 256; v += kParseBlock) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int b = 0; b < 8; ++b)
+                acc ^= (v & (0x80u >> b)) ? P.kwin[8 * j + b] : 0u;
+            tbl[j * 256 + v] = acc;
+        }
+    }
+    if (kCount)
+        for (uint32_t b = lane; b < P.nb; b += kWave)
+            cnt[b] = 0;
+    __syncthreads();
+
+    const uint32_t gw = blockIdx.x * kParseWaves + wave;
+    const uint64_t beg64 = (uint64_t)gw * P.seg;
+    const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
+    const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
+
+    // Staging layout: chunk c (16 B) of tile packet p at uint4 slot
+    // p*4 + (c ^ ((p>>2)&3)).  Writes: lane l holds chunk l&3 of packet
+    // 16k + l/4, so (p>>2)&3 == (l>>4)&3.  Reads: packet p = l, swizzle (l>>2)&3.
+    const uint32_t wsw = (lane >> 4) & 3u;
+    const uint32_t rsw = (lane >> 2) & 3u;
+    const uint32_t *mine = reinterpret_cast<const uint32_t *>(stage + lane * 4);
+
+    for (uint32_t t0 = beg; t0 < end; t0 += kTile) {
+        uint4 r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // clamp instead of branching so every load issues unconditionally
+            const uint32_t pk = min(t0 + 16u * k + (lane >> 2), end - 1u);
+            r[k] = *reinterpret_cast<const uint4 *>(P.win + (size_t)pk * P.stride +
+                                                     (lane & 3u) * 16u);
+        }
+        const uint32_t pkt = t0 + lane;
+        const bool valid = pkt < end;
+        const uint32_t L = valid ? P.len[min(pkt, end - 1u)] : 0u;
+
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            stage[(16u * k + (lane >> 2)) * 4u + ((lane & 3u) ^ wsw)] = r[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        const uint4 c0 = stage[lane * 4 + (0u ^ rsw)];
+        const uint4 c1 = stage[lane * 4 + (1u ^ rsw)];
+        const uint32_t d3 = c0.w;          // bytes 12..15: ether_type, ver/IHL
+        const uint32_t d5 = c1.y;          // bytes 20..23: proto at 23
+        const uint32_t d6 = c1.z;          // bytes 24..27: saddr[0..1] at 26,27
+        const uint32_t d7 = c1.w;          // bytes 28..31: saddr[2..3], daddr[0..1]
+        const uint32_t d8 = mine[((2u ^ rsw) << 2) | 0u];   // bytes 32..35
+        const uint32_t ihl = (d3 >> 16) & 0xfu;
+        const uint32_t ihl4 = ihl << 2;
+
+        // toeplitz_dispatch's checks (ff_dpdk_if.c:1956-1986)
+        const uint32_t et = ((d3 & 0xffu) << 8) | ((d3 >> 8) & 0xffu);
+        int qv = YRSS_DEFAULT_Q;
+        bool hashed = false;
+        if (valid && L >= 14u) {
+            if (et == 0x0800u) {
+                const uint32_t ip_len = L - 14u;
+                hashed = ip_len >= 20u && ip_len >= ihl4 && (L - ihl4) >= 20u &&
+                         (d5 >> 24) == 6u;
+            } else if (et == 0x0806u || et == 0x8035u) {
+                qv = 0;
+            }
+        }
+        uint32_t h = 0;
+        if (hashed) {
+            // TCP ports at p = 14 + 4*IHL: dwords 3+IHL (bytes 2,3) and 4+IHL (0,1).
+            const uint32_t j = 3u + ihl;
+            uint32_t pa, pb;
+            bool trunc = false;
+            if (j + 1u < 16u) {
+                pa = mine[(((j >> 2) ^ rsw) << 2) | (j & 3u)];
+                pb = mine[((((j + 1u) >> 2) ^ rsw) << 2) | ((j + 1u) & 3u)];
+            } else if (18u + ihl4 <= P.stride) {
+                const uint32_t *g = reinterpret_cast<const uint32_t *>(
+                    P.win + (size_t)pkt * P.stride);
+                pa = g[j];
+                pb = g[j + 1u];
+            } else {
+                pa = pb = 0u;
+                trunc = true;
+            }
+            // Tuple = LE image of ntohl(src), ntohl(dst), ntohs(sport), ntohs(dport)
+            // (ff_dpdk_if.c:1994-2021).
+            h = tbl[0 * 256 + ((d7 >> 8) & 0xffu)] ^     // b29
+                tbl[1 * 256 + (d7 & 0xffu)] ^            // b28
+                tbl[2 * 256 + (d6 >> 24)] ^              // b27
+                tbl[3 * 256 + ((d6 >> 16) & 0xffu)] ^    // b26
+                tbl[4 * 256 + ((d8 >> 8) & 0xffu)] ^     // b33
+                tbl[5 * 256 + (d8 & 0xffu)] ^            // b32
+                tbl[6 * 256 + (d7 >> 24)] ^              // b31
+                tbl[7 * 256 + ((d7 >> 16) & 0xffu)] ^    // b30
+                tbl[8 * 256 + (pa >> 24)] ^              // b[p+1]
+                tbl[9 * 256 + ((pa >> 16) & 0xffu)] ^    // b[p]
+                tbl[10 * 256 + ((pb >> 8) & 0xffu)] ^    // b[p+3]
+                tbl[11 * 256 + (pb & 0xffu)];            // b[p+2]
+            // hash % d exactly (Lemire fastmod, 64-bit M), then +q_off (:2031-2034)
+            const uint64_t low = P.mod_m * (uint64_t)h;
+            const uint32_t rem = (uint32_t)__umul64hi(low, (uint64_t)P.mod_d);
+            qv = (int)(uint16_t)(rem + P.q_off);
+            if (trunc) {
+                qv = YRSS_Q_TRUNCATED;
+                h = 0u;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+
+        if (valid) {
+            P.q[pkt] = (int16_t)qv;
+            if (P.hash)
+                P.hash[pkt] = h;
+        }
+
+        if (kCount) {
+            const uint32_t bkt = bucket_of(qv, P.nq);
+            uint64_t pending = __ballot(valid);
+            while (pending) {
+                const int leader = __builtin_ctzll(pending);
+                const uint32_t B = __builtin_amdgcn_readlane(bkt, leader);
+                const uint64_t m = __ballot(valid && bkt == B);
+                if (lane == 0)
+                    cnt[B] += (uint32_t)__popcll(m);
+                pending &= ~m;
+            }
+        }
+    }
+
+    if (kCount) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t b = lane; b < P.nb; b += kWave)
+            P.seg_cnt[(size_t)gw * P.nb + b] = cnt[b];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 2: per-bucket exclusive scan over wave segments.  One workgroup per
+// bucket; segments <= a few thousand.
+// ---------------------------------------------------------------------------
+constexpr int kScanBlock = 1024;
+
+__global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(const uint32_t *seg_cnt,
+                                                            uint32_t *seg_off,
+                                                            uint32_t *totals,
+                                                            uint32_t nseg, uint32_t nb)
+{
+    __shared__ uint32_t wsum[kScanBlock / kWave];
+    const uint32_t b = blockIdx.x;
+    const uint32_t per = (nseg + kScanBlock - 1) / kScanBlock;
+    const uint32_t s0 = threadIdx.x * per;
+    uint32_t local = 0;
+    for (uint32_t s = s0; s < s0 + per && s < nseg; ++s)
+        local += seg_cnt[(size_t)s * nb + b];
+    // inclusive wave scan
+    uint32_t x = local;
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, kWave);
+        if (lane >= (uint32_t)d)
+            x += y;
+    }
+    const uint32_t wave = threadIdx.x / kWave;
+    if (lane == kWave - 1)
+        wsum[wave] = x;
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t v = lane < kScanBlock / kWave ? wsum[lane] : 0u;
+#pragma unroll
+        for (int d = 1; d < kScanBlock / kWave; d <<= 1) {
+            const uint32_t y = __shfl_up(v, d, kWave);
+            if (lane >= (uint32_t)d)
+                v += y;
+        }
+        if (lane < kScanBlock / kWave)
+            wsum[lane] = v;
+    }
+    __syncthreads();
+    uint32_t run = x - local + (wave ? wsum[wave - 1] : 0u);
+    for (uint32_t s = s0; s < s0 + per && s < nseg; ++s) {
+        const uint32_t c = seg_cnt[(size_t)s * nb + b];
+        seg_off[(size_t)s * nb + b] = run;
+        run += c;
+    }
+    if (threadIdx.x == kScanBlock - 1)
+        totals[b] = run;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 3: stable scatter of packet indices into per-bucket lists.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kParseBlock) void yrss_scatter(ScatterParams P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = threadIdx.x / kWave;
+    const uint32_t lane = lane_id();
+    uint32_t *off = reinterpret_cast<uint32_t *>(smem) + wave * P.nb;
+    const uint32_t gw = blockIdx.x * kParseWaves + wave;
+
+    // start[b] = exclusive scan of totals; off[b] = start[b] + seg_off[gw][b]
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+        const uint32_t b = b0 + lane;
+        const uint32_t t = b < P.nb ? P.totals[b] : 0u;
+        uint32_t x = t;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, kWave);
+            if (lane >= (uint32_t)d)
+                x += y;
+        }
+        const uint32_t start = carry + x - t;
+        if (b < P.nb) {
+            off[b] = start + P.seg_off[(size_t)gw * P.nb + b];
+            if (gw == 0)
+                P.qstart[b] = start;
+        }
+        carry += __shfl(x, kWave - 1, kWave);
+    }
+    if (gw == 0 && lane == 0)
+        P.qstart[P.nb] = carry;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    const uint64_t beg64 = (uint64_t)gw * P.seg;
+    const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
+    const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
+
+    for (uint32_t r0 = beg; r0 < end; r0 += kWave * kScatterRound) {
+        uint32_t bk[kScatterRound];
+        uint32_t pend = 0;
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j) {
+            const uint32_t pkt = r0 + j * kWave + lane;
+            bk[j] = bucket_of(P.q[min(pkt, end - 1u)], P.nq);
+            pend |= (pkt < end ? 1u : 0u) << j;
+        }
+        for (;;) {
+            const uint64_t act = __ballot(pend != 0u);
+            if (!act)
+                break;
+            const int leader = __builtin_ctzll(act);
+            uint32_t first = 0;
+#pragma unroll
+            for (int j = kScatterRound - 1; j >= 0; --j)
+                first = ((pend >> j) & 1u) ? bk[j] : first;
+            const uint32_t B = __builtin_amdgcn_readlane(first, leader);
+            const uint32_t base = __builtin_amdgcn_readfirstlane(off[B]);
+            uint32_t run = 0;
+#pragma unroll
+            for (int j = 0; j < kScatterRound; ++j) {
+                const bool take = ((pend >> j) & 1u) && bk[j] == B;
+                const uint64_t m = __ballot(take);
+                if (take)
+                    P.qidx[base + run + rank_below(m)] = r0 + j * kWave + lane;
+                run += (uint32_t)__popcll(m);
+                pend &= ~((take ? 1u : 0u) << j);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0)
+                off[B] = base + run;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic traffic straight into HBM (bench / parity input), one thread per
+// packet.  Bit-identical to oracle_synth() on the host.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void yrss_synth(yrss_synth_params p, uint64_t first,
+                                                  uint32_t n, uint8_t *win,
+                                                  uint32_t stride, uint16_t *len)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    uint32_t w[20];
+    uint16_t L;
+    yrss_synth_window(&p, first + i, w, &L);
+    uint8_t *dst = win + (size_t)i * stride;
+#pragma unroll
+    for (int c = 0; c < 5; ++c)
+        if ((uint32_t)c * 16u < stride)
+            *reinterpret_cast<uint4 *>(dst + c * 16) =
+                make_uint4(w[4 * c], w[4 * c + 1], w[4 * c + 2], w[4 * c + 3]);
+    for (uint32_t c = 5; c * 16u < stride; ++c) {
+        uint32_t v[4];
+        for (int d = 0; d < 4; ++d) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t k = c * 16u + d * 4u + b;
+                x |= ((k * 131u + i) & 0xffu) << (8 * b);
+            }
+            v[d] = x;
+        }
+        *reinterpret_cast<uint4 *>(dst + c * 16) = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    len[i] = L;
+}
+
+}  // namespace
+
+// ===========================================================================
+// Host side
+// ===========================================================================
+
+struct TimedPair {
+    hipEvent_t a, b;
+    int kernel;
+};
+
+struct yrss_ctx {
+    yrss_config cfg;
+    int device = 0;
+    int cus = 0;
+    uint32_t blocks_per_cu = 4;
+    uint32_t nb = 0;
+    ParseParams proto{};        // key schedule, modulo constants
+    // compaction workspace, sized for the grid cap
+    uint32_t seg_cap = 0;
+    uint32_t *d_seg_cnt = nullptr;
+    uint32_t *d_seg_off = nullptr;
+    uint32_t *d_totals = nullptr;
+    // host-burst staging
+    hipStream_t stream = nullptr;
+    uint32_t burst_cap = 0;
+    uint8_t *h_win = nullptr;
+    uint16_t *h_len = nullptr;
+    int16_t *h_q = nullptr;
+    uint32_t *h_hash = nullptr;
+    uint32_t *h_qidx = nullptr;
+    uint32_t *h_qstart = nullptr;
+    uint8_t *d_win = nullptr;
+    uint16_t *d_len = nullptr;
+    int16_t *d_q = nullptr;
+    uint32_t *d_hash = nullptr;
+    uint32_t *d_qidx = nullptr;
+    uint32_t *d_qstart = nullptr;
+    // timing
+    uint32_t timing_mask = 0;    // bit k: bracket kernel k with events
+    std::vector<hipEvent_t> ev_free;
+    std::vector<TimedPair> ev_pending;
+    double ms[YRSS_K_COUNT] = {0, 0, 0};
+    uint32_t launches[YRSS_K_COUNT] = {0, 0, 0};
+};
+
+namespace {
+
+int hip_fail(const char *what, hipError_t e)
+{
+    fprintf(stderr, "yrss: %s failed: %s\n", what, hipGetErrorString(e));
+    return -EIO;
+}
+
+#define YRSS_HIP(call)                                   \
+    do {                                                 \
+        hipError_t e_ = (call);                          \
+        if (e_ != hipSuccess)                            \
+            return hip_fail(#call, e_);                  \
+    } while (0)
+
+uint32_t grid_for(const yrss_ctx *c, uint32_t n)
+{
+    const uint32_t per_block = kParseWaves * kTile;
+    const uint32_t want = (n + per_block - 1) / per_block;
+    const uint32_t cap = (uint32_t)c->cus * c->blocks_per_cu;
+    return std::max(1u, std::min(want, cap));
+}
+
+uint32_t seg_for(uint32_t n, uint32_t grid)
+{
+    const uint32_t waves = grid * kParseWaves;
+    uint32_t s = (n + waves - 1) / waves;
+    s = (s + kTile - 1) / kTile * kTile;
+    return std::max<uint32_t>(s, kTile);
+}
+
+hipEvent_t take_event(yrss_ctx *c)
+{
+    if (c->ev_free.empty()) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess)
+            return nullptr;
+        return e;
+    }
+    hipEvent_t e = c->ev_free.back();
+    c->ev_free.pop_back();
+    return e;
+}
+
+struct Timed {
+    yrss_ctx *c;
+    hipStream_t s;
+    int k;
+    hipEvent_t a = nullptr, b = nullptr;
+    Timed(yrss_ctx *c_, hipStream_t s_, int k_) : c(c_), s(s_), k(k_)
+    {
+        if ((c->timing_mask >> k) & 1u) {
+            a = take_event(c);
+            b = take_event(c);
+            if (a)
+                (void)hipEventRecord(a, s);
+        }
+    }
+    ~Timed()
+    {
+        if (a && b) {
+            (void)hipEventRecord(b, s);
+            c->ev_pending.push_back({a, b, k});
+        }
+    }
+};
+
+void compute_key_schedule(const yrss_config *cfg, uint32_t kwin[96])
+{
+    for (unsigned k = 0; k < 96; ++k) {
+        uint32_t w = 0;
+        for (unsigned b = 0; b < 32; ++b) {
+            const unsigned bit = k + b, kb = bit >> 3;
+            const unsigned v =
+                kb < cfg->rss_key_len ? (cfg->rss_key[kb] >> (7 - (bit & 7))) & 1u : 0u;
+            w = (w << 1) | v;
+        }
+        kwin[k] = w;
+    }
+}
+
+void free_burst(yrss_ctx *c)
+{
+    (void)hipHostFree(c->h_win); (void)hipHostFree(c->h_len); (void)hipHostFree(c->h_q);
+    (void)hipHostFree(c->h_hash); (void)hipHostFree(c->h_qidx); (void)hipHostFree(c->h_qstart);
+    (void)hipFree(c->d_win); (void)hipFree(c->d_len); (void)hipFree(c->d_q);
+    (void)hipFree(c->d_hash); (void)hipFree(c->d_qidx); (void)hipFree(c->d_qstart);
+    c->h_win = nullptr; c->h_len = nullptr; c->h_q = nullptr;
+    c->h_hash = nullptr; c->h_qidx = nullptr; c->h_qstart = nullptr;
+    c->d_win = nullptr; c->d_len = nullptr; c->d_q = nullptr;
+    c->d_hash = nullptr; c->d_qidx = nullptr; c->d_qstart = nullptr;
+    c->burst_cap = 0;
+}
+
+int ensure_burst(yrss_ctx *c, uint32_t n)
+{
+    if (n <= c->burst_cap)
+        return 0;
+    free_burst(c);
+    const uint32_t cap = std::max<uint32_t>(n, 1024u);
+    const size_t nbk = (size_t)c->nb + 1;
+    YRSS_HIP(hipHostMalloc((void **)&c->h_win, (size_t)cap * YRSS_WIN_FULL, hipHostMallocDefault));
+    YRSS_HIP(hipHostMalloc((void **)&c->h_len, (size_t)cap * 2, hipHostMallocDefault));
+    YRSS_HIP(hipHostMalloc((void **)&c->h_q, (size_t)cap * 2, hipHostMallocDefault));
+    YRSS_HIP(hipHostMalloc((void **)&c->h_hash, (size_t)cap * 4, hipHostMallocDefault));
+    YRSS_HIP(hipHostMalloc((void **)&c->h_qidx, (size_t)cap * 4, hipHostMallocDefault));
+    YRSS_HIP(hipHostMalloc((void **)&c->h_qstart, nbk * 4, hipHostMallocDefault));
+    YRSS_HIP(hipMalloc((void **)&c->d_win, (size_t)cap * YRSS_WIN_FULL));
+    YRSS_HIP(hipMalloc((void **)&c->d_len, (size_t)cap * 2));
+    YRSS_HIP(hipMalloc((void **)&c->d_q, (size_t)cap * 2));
+    YRSS_HIP(hipMalloc((void **)&c->d_hash, (size_t)cap * 4));
+    YRSS_HIP(hipMalloc((void **)&c->d_qidx, (size_t)cap * 4));
+    YRSS_HIP(hipMalloc((void **)&c->d_qstart, nbk * 4));
+    c->burst_cap = cap;
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *yrss_version(void) { return YRSS_VERSION_STRING; }
+
+const char *yrss_kernel_name(int k)
+{
+    switch (k) {
+    case YRSS_K_PARSE_HASH: return "yrss_parse_hash";
+    case YRSS_K_SCAN: return "yrss_seg_scan";
+    case YRSS_K_SCATTER: return "yrss_scatter";
+    default: return "";
+    }
+}
+
+void yrss_config_default(struct yrss_config *cfg)
+{
+    // Mellanox Linux driver key, ff_dpdk_if.c:113-119.
+    static const uint8_t mlx_key[YRSS_RSS_KEY_LEN] = {
+        0xd1, 0x81, 0xc6, 0x2c, 0xf7, 0xf4, 0xdb, 0x5b, 0x19, 0x83,
+        0xa2, 0xfc, 0x94, 0x3e, 0x1a, 0xdb, 0xd9, 0x38, 0x9e, 0x6b,
+        0xd1, 0x03, 0x9c, 0x2c, 0xa7, 0x44, 0x99, 0xad, 0x59, 0x3d,
+        0x56, 0xd9, 0xf3, 0x25, 0x3c, 0x06, 0x2a, 0xdc, 0x1f, 0xfc};
+    memset(cfg, 0, sizeof(*cfg));
+    memcpy(cfg->rss_key, mlx_key, sizeof(mlx_key));
+    cfg->rss_key_len = YRSS_RSS_KEY_LEN;
+    cfg->nb_procs = 3;            // fs/config/config.ini lcore_mask=7
+    cfg->nb_queues = 3;
+    cfg->soft_dispatch = 1;       // config.ini soft_dispatch=1
+    cfg->dispatch_only_core = 1;  // config.ini [system] dispatch_only_core=1
+    cfg->device = 0;
+    cfg->max_burst = 1u << 16;
+    cfg->mbuf.off_buf_addr = YRSS_MBUF_OFF_BUF_ADDR;
+    cfg->mbuf.off_data_off = YRSS_MBUF_OFF_DATA_OFF;
+    cfg->mbuf.off_data_len = YRSS_MBUF_OFF_DATA_LEN;
+    cfg->mbuf.off_hash_rss = YRSS_MBUF_OFF_HASH_RSS;
+}
+
+int yrss_config_validate(const struct yrss_config *cfg)
+{
+    if (!cfg)
+        return -EINVAL;
+    if (cfg->rss_key_len < 4 || cfg->rss_key_len > YRSS_RSS_KEY_LEN)
+        return -EINVAL;
+    if (cfg->nb_procs < 1 || cfg->nb_procs > YRSS_MAX_PROCS)
+        return -EINVAL;
+    if (cfg->nb_queues < 1 || cfg->nb_queues > YRSS_MAX_QUEUES)
+        return -EINVAL;
+    if (cfg->soft_dispatch > 1 || cfg->dispatch_only_core > 1)
+        return -EINVAL;
+    // hash % (nb_procs - 1) would divide by zero (ff_dpdk_if.c:2032)
+    if (cfg->soft_dispatch && cfg->dispatch_only_core && cfg->nb_procs < 2)
+        return -EINVAL;
+    if (cfg->device < 0)
+        return -EINVAL;
+    return 0;
+}
+
+int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
+{
+    if (!out)
+        return -EINVAL;
+    *out = nullptr;
+    int rc = yrss_config_validate(cfg);
+    if (rc)
+        return rc;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device)
+        return -ENODEV;
+    YRSS_HIP(hipSetDevice(cfg->device));
+    hipDeviceProp_t prop;
+    YRSS_HIP(hipGetDeviceProperties(&prop, cfg->device));
+
+    yrss_ctx *c = new (std::nothrow) yrss_ctx();
+    if (!c)
+        return -ENOMEM;
+    c->cfg = *cfg;
+    c->device = cfg->device;
+    c->cus = prop.multiProcessorCount;
+    if (const char *e = getenv("YRSS_BLOCKS_PER_CU")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 16)
+            c->blocks_per_cu = (uint32_t)v;
+    }
+    c->nb = (uint32_t)cfg->nb_queues + 1u;
+    compute_key_schedule(cfg, c->proto.kwin);
+    const bool only = cfg->soft_dispatch && cfg->dispatch_only_core;
+    c->proto.mod_d = (uint32_t)(only ? cfg->nb_procs - 1 : cfg->nb_procs);
+    c->proto.q_off = only ? 1u : 0u;
+    c->proto.mod_m = UINT64_MAX / c->proto.mod_d + 1u;   // wraps to 0 for d == 1
+    c->proto.nq = cfg->nb_queues;
+    c->proto.nb = c->nb;
+
+    c->seg_cap = (uint32_t)c->cus * c->blocks_per_cu * kParseWaves;
+    const size_t ws = (size_t)c->seg_cap * c->nb * sizeof(uint32_t);
+    hipError_t e;
+    if ((e = hipMalloc((void **)&c->d_seg_cnt, ws)) != hipSuccess ||
+        (e = hipMalloc((void **)&c->d_seg_off, ws)) != hipSuccess ||
+        (e = hipMalloc((void **)&c->d_totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+        yrss_fini(c);
+        return hip_fail("yrss_init allocation", e);
+    }
+    if (cfg->max_burst && (rc = ensure_burst(c, cfg->max_burst)) != 0) {
+        yrss_fini(c);
+        return rc;
+    }
+    *out = c;
+    return 0;
+}
+
+void yrss_fini(yrss_ctx *c)
+{
+    if (!c)
+        return;
+    (void)hipSetDevice(c->device);
+    if (c->stream)
+        (void)hipStreamSynchronize(c->stream);
+    for (auto &p : c->ev_pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : c->ev_free)
+        (void)hipEventDestroy(e);
+    free_burst(c);
+    (void)hipFree(c->d_seg_cnt);
+    (void)hipFree(c->d_seg_off);
+    (void)hipFree(c->d_totals);
+    if (c->stream)
+        (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+uint32_t yrss_grid_for(yrss_ctx *c, uint32_t n) { return c ? grid_for(c, n) : 0u; }
+
+int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
+                      const uint16_t *d_len, uint32_t n, int16_t *d_q, uint32_t *d_hash,
+                      uint32_t *d_qidx, uint32_t *d_qstart, void *stream)
+{
+    if (!c)
+        return -EINVAL;
+    if (win_stride < YRSS_WIN_MIN || (win_stride & 15u))
+        return -EINVAL;
+    if (n && (!d_win || !d_len || !d_q))
+        return -EINVAL;
+    if (((uintptr_t)d_win & 15u) || ((uintptr_t)d_len & 1u) || ((uintptr_t)d_q & 1u) ||
+        ((uintptr_t)d_hash & 3u) || ((uintptr_t)d_qidx & 3u) || ((uintptr_t)d_qstart & 3u))
+        return -EINVAL;
+    const bool compact = d_qidx != nullptr;
+    if (compact && !d_qstart)
+        return -EINVAL;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        if (compact)
+            YRSS_HIP(hipMemsetAsync(d_qstart, 0, (c->nb + 1) * sizeof(uint32_t), s));
+        return 0;
+    }
+
+    const uint32_t grid = grid_for(c, n);
+    const uint32_t seg = seg_for(n, grid);
+    const uint32_t nseg = grid * kParseWaves;
+
+    ParseParams P = c->proto;
+    P.win = d_win;
+    P.len = d_len;
+    P.q = d_q;
+    P.hash = d_hash;
+    P.seg_cnt = compact ? c->d_seg_cnt : nullptr;
+    P.n = n;
+    P.stride = win_stride;
+    P.seg = seg;
+    const size_t lds = kTblBytes + kParseWaves * kStageBytes +
+                       (size_t)kParseWaves * c->nb * sizeof(uint32_t);
+    {
+        Timed t(c, s, YRSS_K_PARSE_HASH);
+        if (compact)
+            hipLaunchKernelGGL(yrss_parse_hash<true>, dim3(grid), dim3(kParseBlock), lds, s, P);
+        else
+            hipLaunchKernelGGL(yrss_parse_hash<false>, dim3(grid), dim3(kParseBlock), lds, s, P);
+    }
+    YRSS_HIP(hipGetLastError());
+    if (!compact)
+        return 0;
+    {
+        Timed t(c, s, YRSS_K_SCAN);
+        hipLaunchKernelGGL(yrss_seg_scan, dim3(c->nb), dim3(kScanBlock), 0, s,
+                           (const uint32_t *)c->d_seg_cnt, c->d_seg_off, c->d_totals,
+                           nseg, c->nb);
+    }
+    YRSS_HIP(hipGetLastError());
+    ScatterParams S;
+    S.q = d_q;
+    S.seg_off = c->d_seg_off;
+    S.totals = c->d_totals;
+    S.qidx = d_qidx;
+    S.qstart = d_qstart;
+    S.n = n;
+    S.seg = seg;
+    S.nq = c->cfg.nb_queues;
+    S.nb = c->nb;
+    {
+        Timed t(c, s, YRSS_K_SCATTER);
+        hipLaunchKernelGGL(yrss_scatter, dim3(grid), dim3(kParseBlock),
+                           (size_t)kParseWaves * c->nb * sizeof(uint32_t), s, S);
+    }
+    YRSS_HIP(hipGetLastError());
+    return 0;
+}
+
+static int burst_common(yrss_ctx *c, uint32_t n, uint32_t wstride, int16_t *out_q,
+                        uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart)
+{
+    hipStream_t s = c->stream;
+    const bool compact = out_qidx && out_qstart;
+    YRSS_HIP(hipMemcpyAsync(c->d_win, c->h_win, (size_t)n * wstride, hipMemcpyHostToDevice, s));
+    YRSS_HIP(hipMemcpyAsync(c->d_len, c->h_len, (size_t)n * 2, hipMemcpyHostToDevice, s));
+    int rc = yrss_dispatch_dev(c, c->d_win, wstride, c->d_len, n, c->d_q,
+                               out_hash ? c->d_hash : nullptr, compact ? c->d_qidx : nullptr,
+                               compact ? c->d_qstart : nullptr, s);
+    if (rc)
+        return rc;
+    YRSS_HIP(hipMemcpyAsync(c->h_q, c->d_q, (size_t)n * 2, hipMemcpyDeviceToHost, s));
+    if (out_hash)
+        YRSS_HIP(hipMemcpyAsync(c->h_hash, c->d_hash, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (compact) {
+        YRSS_HIP(hipMemcpyAsync(c->h_qidx, c->d_qidx, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        YRSS_HIP(hipMemcpyAsync(c->h_qstart, c->d_qstart, (c->nb + 1) * 4,
+                                hipMemcpyDeviceToHost, s));
+    }
+    YRSS_HIP(hipStreamSynchronize(s));
+    memcpy(out_q, c->h_q, (size_t)n * 2);
+    if (out_hash)
+        memcpy(out_hash, c->h_hash, (size_t)n * 4);
+    if (compact) {
+        memcpy(out_qidx, c->h_qidx, (size_t)n * 4);
+        memcpy(out_qstart, c->h_qstart, (c->nb + 1) * 4);
+    }
+    return 0;
+}
+
+int yrss_dispatch_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t *len,
+                         uint32_t n, int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx,
+                         uint32_t *out_qstart)
+{
+    if (!c || (n && (!data || !len || !out_q)))
+        return -EINVAL;
+    if (n == 0) {
+        if (out_qstart)
+            memset(out_qstart, 0, (c->nb + 1) * sizeof(uint32_t));
+        return 0;
+    }
+    YRSS_HIP(hipSetDevice(c->device));
+    int rc = ensure_burst(c, n);
+    if (rc)
+        return rc;
+    uint32_t maxlen = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        maxlen = std::max<uint32_t>(maxlen, len[i]);
+    const uint32_t W = maxlen <= YRSS_WIN_MIN ? YRSS_WIN_MIN : YRSS_WIN_FULL;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t L = len[i];
+        memcpy(c->h_win + (size_t)i * W, data[i], L < W ? L : W);
+        c->h_len[i] = (uint16_t)L;
+    }
+    return burst_common(c, n, W, out_q, out_hash, out_qidx, out_qstart);
+}
+
+int yrss_dispatch_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out_q,
+                        uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                        uint32_t flags)
+{
+    if (!c || (n && (!mbufs || !out_q)))
+        return -EINVAL;
+    if (n == 0) {
+        if (out_qstart)
+            memset(out_qstart, 0, (c->nb + 1) * sizeof(uint32_t));
+        return 0;
+    }
+    YRSS_HIP(hipSetDevice(c->device));
+    int rc = ensure_burst(c, n);
+    if (rc)
+        return rc;
+    const yrss_mbuf_layout &ml = c->cfg.mbuf;
+    uint32_t maxlen = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *m = (const uint8_t *)mbufs[i];
+        uint16_t L;
+        memcpy(&L, m + ml.off_data_len, 2);
+        c->h_len[i] = L;
+        maxlen = std::max<uint32_t>(maxlen, L);
+    }
+    const uint32_t W = maxlen <= YRSS_WIN_MIN ? YRSS_WIN_MIN : YRSS_WIN_FULL;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *m = (const uint8_t *)mbufs[i];
+        const uint8_t *buf;
+        uint16_t doff;
+        memcpy(&buf, m + ml.off_buf_addr, sizeof(buf));
+        memcpy(&doff, m + ml.off_data_off, 2);     // rte_pktmbuf_mtod, rte_mbuf.h:1620
+        const uint32_t L = c->h_len[i];
+        memcpy(c->h_win + (size_t)i * W, buf + doff, L < W ? L : W);
+    }
+    uint32_t *hash = out_hash;
+    std::vector<uint32_t> tmp;
+    if (!hash && (flags & YRSS_F_WRITE_RSS)) {
+        tmp.resize(n);
+        hash = tmp.data();
+    }
+    rc = burst_common(c, n, W, out_q, hash, out_qidx, out_qstart);
+    if (rc)
+        return rc;
+    if (flags & YRSS_F_WRITE_RSS)
+        for (uint32_t i = 0; i < n; ++i)
+            memcpy((uint8_t *)mbufs[i] + ml.off_hash_rss, &hash[i], 4);
+    return 0;
+}
+
+int yrss_synth_dev(yrss_ctx *c, const struct yrss_synth_params *p, uint64_t first, uint32_t n,
+                   uint8_t *d_win, uint32_t win_stride, uint16_t *d_len, void *stream)
+{
+    if (!c || !p || p->profile >= YRSS_SYN_NPROFILES)
+        return -EINVAL;
+    if (win_stride < YRSS_WIN_MIN || (win_stride & 15u) || ((uintptr_t)d_win & 15u))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    hipLaunchKernelGGL(yrss_synth, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       *p, first, n, d_win, win_stride, d_len);
+    YRSS_HIP(hipGetLastError());
+    return 0;
+}
+
+int yrss_timing_enable(yrss_ctx *c, int enable)
+{
+    if (!c)
+        return -EINVAL;
+    yrss_timing_read(c, 0, nullptr, nullptr);   // drain pending pairs
+    c->timing_mask = (uint32_t)enable & ((1u << YRSS_K_COUNT) - 1u);
+    for (int k = 0; k < YRSS_K_COUNT; ++k) {
+        c->ms[k] = 0.0;
+        c->launches[k] = 0;
+    }
+    return 0;
+}
+
+int yrss_timing_read(yrss_ctx *c, int kernel, double *total_ms, uint32_t *launches)
+{
+    if (!c || kernel < 0 || kernel >= YRSS_K_COUNT)
+        return -EINVAL;
+    for (auto &p : c->ev_pending) {
+        YRSS_HIP(hipEventSynchronize(p.b));
+        float ms = 0.f;
+        YRSS_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+        c->ms[p.kernel] += ms;
+        c->launches[p.kernel] += 1;
+        c->ev_free.push_back(p.a);
+        c->ev_free.push_back(p.b);
+    }
+    c->ev_pending.clear();
+    if (total_ms)
+        *total_ms = c->ms[kernel];
+    if (launches)
+        *launches = c->launches[kernel];
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,208 @@
+"""Host-side mirror of yastack's dispatch interface over the HIP engine.
+
+Reference interface (fs/lib/ff_api.h:146-176, fs/lib/ff_dpdk_if.c):
+
+* ``toeplitz_dispatch(data, len, queue_id, nb_queues) -> int`` — per packet.
+  Here: :meth:`SoftRss.dispatch_frames` / :meth:`SoftRss.dispatch_burst`
+  return the same per-packet ints for a whole burst, computed on the GPU.
+* ``process_packets``' dispatcher block (ff_dpdk_if.c:1078-1094) — drop
+  ``ret < 0 || ret >= nb_queues``, else enqueue to ``dispatch_ring[port][ret]``.
+  Here: the per-queue FIFO index lists of :class:`DispatchResult`.
+* ``ff_global_cfg`` knobs (nb_procs, soft_dispatch, dispatch_only_core) and the
+  port's nb_queues: the :class:`SoftRss` constructor, or
+  :meth:`SoftRss.from_ff_config` for an fs/lib INI file.
+
+Device memory and streams come from PyTorch (plumbing only); every byte of
+parse/hash/compaction runs in the HIP kernels of libyrss.so.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import abi
+
+
+@dataclass
+class DispatchResult:
+    """Per-packet queue/hash plus per-queue FIFO index lists.
+
+    ``q[i]``      toeplitz_dispatch's return for packet i (int16)
+    ``hash[i]``   Toeplitz hash (0 where the reference does not hash)
+    ``qidx``      packet indices grouped by bucket, FIFO inside a bucket
+    ``qstart``    nb_queues+2 offsets; bucket nb_queues = packets the
+                  reference frees (ret < 0 or ret >= nb_queues)
+    """
+
+    q: object
+    hash: object
+    qidx: object = None
+    qstart: object = None
+
+    def queue(self, b: int):
+        """Indices dispatched to queue b (b == nb_queues: dropped)."""
+        s = self.qstart
+        return self.qidx[int(s[b]):int(s[b + 1])]
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data
+    return t.data_ptr()
+
+
+class SoftRss:
+    """One engine context on one GPU (``yrss_ctx``)."""
+
+    def __init__(self, nb_procs: int = 3, nb_queues: int | None = None,
+                 soft_dispatch: int = 1, dispatch_only_core: int = 1,
+                 rss_key: bytes | None = None, device: int = 0,
+                 max_burst: int = 1 << 16):
+        self._lib = abi.load()
+        cfg = abi.default_config()
+        if rss_key is not None:
+            if not 4 <= len(rss_key) <= abi.RSS_KEY_LEN:
+                raise ValueError("rss_key must be 4..40 bytes")
+            ctypes.memmove(cfg.rss_key, bytes(rss_key), len(rss_key))
+            cfg.rss_key_len = len(rss_key)
+        cfg.nb_procs = nb_procs
+        cfg.nb_queues = nb_procs if nb_queues is None else nb_queues
+        cfg.soft_dispatch = soft_dispatch
+        cfg.dispatch_only_core = dispatch_only_core
+        cfg.device = device
+        cfg.max_burst = max_burst
+        self.cfg = cfg
+        self.nb_queues = int(cfg.nb_queues)
+        self.device = device
+        ctx = ctypes.c_void_p()
+        abi.check(self._lib.yrss_init(ctypes.byref(cfg), ctypes.byref(ctx)), "yrss_init")
+        self._ctx = ctx
+
+    @classmethod
+    def from_ff_config(cls, path: str, port: int = 0, device: int = 0, **kw) -> "SoftRss":
+        from .ffconfig import load_ff_config
+
+        fc = load_ff_config(path)
+        return cls(nb_procs=fc.nb_procs, nb_queues=fc.nb_queues[port],
+                   soft_dispatch=fc.soft_dispatch,
+                   dispatch_only_core=fc.dispatch_only_core, device=device, **kw)
+
+    # -- lifetime ---------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self._lib.yrss_fini(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- torch plumbing ------------------------------------------------------
+    def _torch(self):
+        import torch
+
+        return torch
+
+    def _stream(self, stream):
+        torch = self._torch()
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        return ctypes.c_void_p(stream.cuda_stream)
+
+    # -- device-resident path ---------------------------------------------
+    def dispatch_dev(self, win, lens, stride: int, n: int | None = None, *,
+                     out=None, want_hash: bool = True, compact: bool = True,
+                     stream=None) -> DispatchResult:
+        """Classify n packets resident in HBM (``yrss_dispatch_dev``)."""
+        torch = self._torch()
+        n = int(lens.numel()) if n is None else n
+        dev = lens.device
+        if out is None:
+            out = self.alloc_out(n, dev, want_hash, compact)
+        rc = self._lib.yrss_dispatch_dev(
+            self._ctx, _ptr(win), stride, _ptr(lens), n, _ptr(out.q),
+            _ptr(out.hash), _ptr(out.qidx), _ptr(out.qstart), self._stream(stream))
+        abi.check(rc, "yrss_dispatch_dev")
+        return out
+
+    def alloc_out(self, n: int, dev, want_hash=True, compact=True) -> DispatchResult:
+        torch = self._torch()
+        q = torch.empty(max(n, 1), dtype=torch.int16, device=dev)
+        h = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if want_hash else None
+        qi = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if compact else None
+        qs = torch.empty(self.nb_queues + 2, dtype=torch.int32, device=dev) if compact else None
+        return DispatchResult(q, h, qi, qs)
+
+    def synth(self, profile: int, n: int, first: int = 0, seed: int = 0x9E3779B97F4A7C15,
+              nflows: int = 1 << 20, stride: int = abi.WIN_MIN, stream=None):
+        """Synthetic header windows + data_len written straight into HBM."""
+        torch = self._torch()
+        dev = torch.device("cuda", self.device)
+        win = torch.empty(max(n, 1) * stride, dtype=torch.uint8, device=dev)
+        lens = torch.empty(max(n, 1), dtype=torch.int16, device=dev)
+        p = abi.SynthParams(seed & 0xFFFFFFFFFFFFFFFF, profile, nflows)
+        rc = self._lib.yrss_synth_dev(self._ctx, ctypes.byref(p), first, n, _ptr(win), stride,
+                                      _ptr(lens), self._stream(stream))
+        abi.check(rc, "yrss_synth_dev")
+        return win, lens[:n] if n else lens[:0]
+
+    # -- host-resident paths (synchronous) ----------------------------------
+    def dispatch_frames(self, frames, want_hash=True, compact=True) -> DispatchResult:
+        """Classify a list of frames (bytes) — one toeplitz_dispatch per frame."""
+        n = len(frames)
+        bufs = [np.frombuffer(bytes(f), dtype=np.uint8) if len(f) else np.zeros(1, np.uint8)
+                for f in frames]
+        ptrs = np.array([b.ctypes.data for b in bufs], dtype=np.uint64)
+        lens = np.array([len(f) for f in frames], dtype=np.uint16)
+        if np.any(lens != np.array([len(f) for f in frames])):
+            raise ValueError("frame longer than 65535 bytes")
+        q = np.empty(max(n, 1), np.int16)
+        h = np.empty(max(n, 1), np.uint32) if want_hash else None
+        qi = np.empty(max(n, 1), np.uint32) if compact else None
+        qs = np.empty(self.nb_queues + 2, np.uint32) if compact else None
+        rc = self._lib.yrss_dispatch_frames(self._ctx, _ptr(ptrs), _ptr(lens), n, _ptr(q),
+                                            _ptr(h), _ptr(qi), _ptr(qs))
+        abi.check(rc, "yrss_dispatch_frames")
+        return DispatchResult(q[:n], None if h is None else h[:n],
+                              None if qi is None else qi[:n], qs)
+
+    def dispatch_burst(self, mbuf_ptrs: np.ndarray, want_hash=True, compact=True,
+                       write_rss=False) -> DispatchResult:
+        """Classify a burst of ``struct rte_mbuf *`` (uint64 addresses)."""
+        mb = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
+        n = int(mb.size)
+        q = np.empty(max(n, 1), np.int16)
+        h = np.empty(max(n, 1), np.uint32) if want_hash else None
+        qi = np.empty(max(n, 1), np.uint32) if compact else None
+        qs = np.empty(self.nb_queues + 2, np.uint32) if compact else None
+        rc = self._lib.yrss_dispatch_burst(self._ctx, _ptr(mb), n, _ptr(q), _ptr(h), _ptr(qi),
+                                           _ptr(qs), abi.F_WRITE_RSS if write_rss else 0)
+        abi.check(rc, "yrss_dispatch_burst")
+        return DispatchResult(q[:n], None if h is None else h[:n],
+                              None if qi is None else qi[:n], qs)
+
+    # -- timing hook --------------------------------------------------------
+    def timing_enable(self, on: bool = True) -> None:
+        abi.check(self._lib.yrss_timing_enable(self._ctx, 1 if on else 0), "yrss_timing_enable")
+
+    def timing_read(self, kernel: int) -> tuple[float, int]:
+        ms = ctypes.c_double()
+        cnt = ctypes.c_uint32()
+        abi.check(self._lib.yrss_timing_read(self._ctx, kernel, ctypes.byref(ms),
+                                             ctypes.byref(cnt)), "yrss_timing_read")
+        return ms.value, cnt.value
+
+    def grid_for(self, n: int) -> int:
+        return int(self._lib.yrss_grid_for(self._ctx, n))
