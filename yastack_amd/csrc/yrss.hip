@@ -42,8 +42,9 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kTile = 64;              // packets per wave-tile (one per lane)
-constexpr int kParseBlock = 256;       // 4 waves per workgroup
-constexpr int kParseWaves = kParseBlock / kWave;
+constexpr int kScatterBlock = 256;     // 4 waves (segments) per workgroup
+constexpr int kScatterWaves = kScatterBlock / kWave;
+constexpr int kMaxWavesPerCU = 32;
 constexpr int kScatterRound = 8;       // packets per lane per scatter round
 constexpr int kTblBytes = 12 * 256 * 4;
 constexpr int kStageBytes = kTile * 64; // 4 KiB per wave
@@ -95,149 +96,201 @@ __device__ __forceinline__ uint32_t bucket_of(int qv, uint32_t nq)
 // ---------------------------------------------------------------------------
 // Kernel 1: parse + Toeplitz hash + queue, one lane per packet.
 // ---------------------------------------------------------------------------
-template <bool kCount>
-__global__ __launch_bounds__(kParseBlock) void yrss_parse_hash(ParseParams P)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// One 64-packet tile's global loads: four 16-byte chunks per lane (lane l gets
+// chunk l&3 of packet t0 + 16k + l/4, i.e. 1 KiB contiguous per instruction at
+// stride 64) plus the lane's own data_len.  Addresses are clamped to the last
+// packet of the segment instead of branching, so every load always issues and
+// hipcc's vmcnt accounting stays exact across the prefetch.
+template <bool kNT>
+__device__ __forceinline__ void load_tile(const ParseParams &P, uint32_t t0, uint32_t end,
+                                          uint32_t lane, u32x4 (&r)[4], uint32_t &L)
 {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t pk = min(t0 + 16u * k + (lane >> 2), end - 1u);
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(P.win + (size_t)pk * P.stride +
+                                                           (lane & 3u) * 16u);
+        r[k] = kNT ? __builtin_nontemporal_load(src) : *src;
+    }
+    L = P.len[min(t0 + lane, end - 1u)];
+}
+
+template <bool kCount>
+__device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_t *tbl,
+                                             u32x4 *stage, uint32_t *cnt, uint32_t t0,
+                                             uint32_t end, uint32_t lane, const u32x4 (&r)[4],
+                                             uint32_t Lraw)
+{
+    // Staging layout: chunk c (16 B) of tile packet p at slot p*4 + (c ^ ((p>>2)&3)).
+    // Writes: lane l holds chunk l&3 of packet 16k + l/4, so (p>>2)&3 == (l>>4)&3.
+    // Reads: packet p = l, swizzle (l>>2)&3.  Both sides are bank-conflict free
+    // (ds_write_b128 8-lane groups cover 128 contiguous bytes; ds_read_b128
+    // 16-lane groups hit 16 distinct 16-byte slots).
+    const uint32_t wsw = (lane >> 4) & 3u;
+    const uint32_t rsw = (lane >> 2) & 3u;
+    const uint32_t *mine = reinterpret_cast<const uint32_t *>(stage + lane * 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        stage[(16u * k + (lane >> 2)) * 4u + ((lane & 3u) ^ wsw)] = r[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    const uint32_t pkt = t0 + lane;
+    const bool valid = pkt < end;
+    const uint32_t L = valid ? Lraw : 0u;
+    const u32x4 c0 = stage[lane * 4 + (0u ^ rsw)];
+    const u32x4 c1 = stage[lane * 4 + (1u ^ rsw)];
+    const uint32_t d3 = c0.w;          // bytes 12..15: ether_type, ver/IHL
+    const uint32_t d5 = c1.y;          // bytes 20..23: proto at 23
+    const uint32_t d6 = c1.z;          // bytes 24..27: saddr[0..1] at 26,27
+    const uint32_t d7 = c1.w;          // bytes 28..31: saddr[2..3], daddr[0..1]
+    const uint32_t d8 = mine[((2u ^ rsw) << 2) | 0u];   // bytes 32..35
+    const uint32_t ihl = (d3 >> 16) & 0xfu;
+    const uint32_t ihl4 = ihl << 2;
+
+    // toeplitz_dispatch's checks (ff_dpdk_if.c:1956-1986)
+    const uint32_t et = ((d3 & 0xffu) << 8) | ((d3 >> 8) & 0xffu);
+    int qv = YRSS_DEFAULT_Q;
+    bool hashed = false;
+    if (valid && L >= 14u) {
+        if (et == 0x0800u) {
+            const uint32_t ip_len = L - 14u;
+            hashed = ip_len >= 20u && ip_len >= ihl4 && (L - ihl4) >= 20u && (d5 >> 24) == 6u;
+        } else if (et == 0x0806u || et == 0x8035u) {
+            qv = 0;
+        }
+    }
+    uint32_t h = 0;
+    if (hashed) {
+        // TCP ports at p = 14 + 4*IHL: dwords 3+IHL (bytes 2,3) and 4+IHL (0,1).
+        // IHL <= 11 keeps them inside the staged 64 bytes; IHL >= 12 needs
+        // bytes 64..77 and takes the slow path below.
+        const uint32_t j = 3u + ihl;
+        const bool tail = j + 1u >= 16u;
+        const uint32_t jj = tail ? 3u : j;
+        const uint32_t pa = mine[(((jj >> 2) ^ rsw) << 2) | (jj & 3u)];
+        const uint32_t pb = mine[((((jj + 1u) >> 2) ^ rsw) << 2) | ((jj + 1u) & 3u)];
+        // Tuple = LE image of ntohl(src), ntohl(dst), ntohs(sport), ntohs(dport)
+        // (ff_dpdk_if.c:1994-2021); 12 byte-table lookups = bit-serial Toeplitz.
+        const uint32_t h_l3 =
+            tbl[0 * 256 + ((d7 >> 8) & 0xffu)] ^     // b29
+            tbl[1 * 256 + (d7 & 0xffu)] ^            // b28
+            tbl[2 * 256 + (d6 >> 24)] ^              // b27
+            tbl[3 * 256 + ((d6 >> 16) & 0xffu)] ^    // b26
+            tbl[4 * 256 + ((d8 >> 8) & 0xffu)] ^     // b33
+            tbl[5 * 256 + (d8 & 0xffu)] ^            // b32
+            tbl[6 * 256 + (d7 >> 24)] ^              // b31
+            tbl[7 * 256 + ((d7 >> 16) & 0xffu)];     // b30
+        h = h_l3 ^
+            tbl[8 * 256 + (pa >> 24)] ^              // b[p+1]
+            tbl[9 * 256 + ((pa >> 16) & 0xffu)] ^    // b[p]
+            tbl[10 * 256 + ((pb >> 8) & 0xffu)] ^    // b[p+3]
+            tbl[11 * 256 + (pb & 0xffu)];            // b[p+2]
+        bool trunc = false;
+        // Rare slow path, entered only by waves that hold such a packet, so its
+        // global loads (and the vmcnt drain they imply) stay off the hot loop.
+        if (__builtin_expect(tail, 0)) {
+            if (18u + ihl4 <= P.stride) {
+                const uint32_t *g =
+                    reinterpret_cast<const uint32_t *>(P.win + (size_t)pkt * P.stride);
+                const uint32_t ta = __builtin_nontemporal_load(g + j);
+                const uint32_t tb = __builtin_nontemporal_load(g + j + 1u);
+                h = h_l3 ^ tbl[8 * 256 + (ta >> 24)] ^ tbl[9 * 256 + ((ta >> 16) & 0xffu)] ^
+                    tbl[10 * 256 + ((tb >> 8) & 0xffu)] ^ tbl[11 * 256 + (tb & 0xffu)];
+            } else {
+                trunc = true;
+            }
+        }
+        // hash % d exactly (Lemire fastmod, 64-bit M), then +q_off (:2031-2034)
+        const uint64_t low = P.mod_m * (uint64_t)h;
+        const uint32_t rem = (uint32_t)__umul64hi(low, (uint64_t)P.mod_d);
+        qv = (int)(uint16_t)(rem + P.q_off);
+        if (trunc) {
+            qv = YRSS_Q_TRUNCATED;
+            h = 0u;
+        }
+    }
+    // the next tile's ds_writes must not overtake this tile's ds_reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+
+    if (valid) {
+        P.q[pkt] = (int16_t)qv;
+        if (P.hash)
+            P.hash[pkt] = h;
+    }
+
+    if (kCount) {
+        const uint32_t bkt = bucket_of(qv, P.nq);
+        uint64_t pending = __ballot(valid);
+        while (pending) {
+            const int leader = __builtin_ctzll(pending);
+            const uint32_t B = __builtin_amdgcn_readlane(bkt, leader);
+            const uint64_t m = __ballot(valid && bkt == B);
+            if (lane == 0)
+                cnt[B] += (uint32_t)__popcll(m);
+            pending &= ~m;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 1: parse + Toeplitz hash + queue, one lane per packet.
+//   kCount   also count packets per bucket per wave segment (compaction on)
+//   kUnroll  tiles whose loads are all issued before the first is processed
+//            (1 or 2; no loaded register is carried across iterations, so
+//            hipcc's vmcnt accounting never has to drain early)
+//   kNT      non-temporal (streaming) window loads
+//   kBlock   workgroup size (256/512/1024): more waves per CU, more bytes in
+//            flight, one 12 KiB table per workgroup
+// ---------------------------------------------------------------------------
+template <bool kCount, int kUnroll, bool kNT, int kBlock>
+__global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
+{
+    constexpr int kWaves = kBlock / kWave;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t *tbl = reinterpret_cast<uint32_t *>(smem);
     const uint32_t wave = threadIdx.x / kWave;
     const uint32_t lane = lane_id();
-    uint4 *stage = reinterpret_cast<uint4 *>(smem + kTblBytes + wave * kStageBytes);
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + kTblBytes + kParseWaves * kStageBytes) +
+    u32x4 *stage = reinterpret_cast<u32x4 *>(smem + kTblBytes + wave * kStageBytes);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + kTblBytes + kWaves * kStageBytes) +
                     wave * P.nb;
 
+    const uint32_t gw = blockIdx.x * kWaves + wave;
+    const uint64_t beg64 = (uint64_t)gw * P.seg;
+    const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
+    const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
+
     // Byte tables: tbl[j*256+v] = XOR of key windows at bits 8j+b, v's bit b set.
+    for (uint32_t e = threadIdx.x; e < 12u * 256u; e += kBlock) {
+        const uint32_t j = e >> 8, v = e & 255u;
+        uint32_t acc = 0;
 #pragma unroll
-    for (int j = 0; j < 12; ++j) {
-        for (uint32_t v = threadIdx.x; v < 256; v += kParseBlock) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int b = 0; b < 8; ++b)
-                acc ^= (v & (0x80u >> b)) ? P.kwin[8 * j + b] : 0u;
-            tbl[j * 256 + v] = acc;
-        }
+        for (int b = 0; b < 8; ++b)
+            acc ^= (v & (0x80u >> b)) ? P.kwin[8 * j + b] : 0u;
+        tbl[e] = acc;
     }
     if (kCount)
         for (uint32_t b = lane; b < P.nb; b += kWave)
             cnt[b] = 0;
     __syncthreads();
 
-    const uint32_t gw = blockIdx.x * kParseWaves + wave;
-    const uint64_t beg64 = (uint64_t)gw * P.seg;
-    const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
-    const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
-
-    // Staging layout: chunk c (16 B) of tile packet p at uint4 slot
-    // p*4 + (c ^ ((p>>2)&3)).  Writes: lane l holds chunk l&3 of packet
-    // 16k + l/4, so (p>>2)&3 == (l>>4)&3.  Reads: packet p = l, swizzle (l>>2)&3.
-    const uint32_t wsw = (lane >> 4) & 3u;
-    const uint32_t rsw = (lane >> 2) & 3u;
-    const uint32_t *mine = reinterpret_cast<const uint32_t *>(stage + lane * 4);
-
-    for (uint32_t t0 = beg; t0 < end; t0 += kTile) {
-        uint4 r[4];
+    for (uint32_t t0 = beg; t0 < end; t0 += kUnroll * kTile) {
+        u32x4 r[kUnroll][4];
+        uint32_t L[kUnroll];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            // clamp instead of branching so every load issues unconditionally
-            const uint32_t pk = min(t0 + 16u * k + (lane >> 2), end - 1u);
-            r[k] = *reinterpret_cast<const uint4 *>(P.win + (size_t)pk * P.stride +
-                                                     (lane & 3u) * 16u);
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint32_t tu = t0 + u * kTile;
+            load_tile<kNT>(P, tu < end ? tu : t0, end, lane, r[u], L[u]);
         }
-        const uint32_t pkt = t0 + lane;
-        const bool valid = pkt < end;
-        const uint32_t L = valid ? P.len[min(pkt, end - 1u)] : 0u;
-
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            stage[(16u * k + (lane >> 2)) * 4u + ((lane & 3u) ^ wsw)] = r[k];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-        const uint4 c0 = stage[lane * 4 + (0u ^ rsw)];
-        const uint4 c1 = stage[lane * 4 + (1u ^ rsw)];
-        const uint32_t d3 = c0.w;          // bytes 12..15: ether_type, ver/IHL
-        const uint32_t d5 = c1.y;          // bytes 20..23: proto at 23
-        const uint32_t d6 = c1.z;          // bytes 24..27: saddr[0..1] at 26,27
-        const uint32_t d7 = c1.w;          // bytes 28..31: saddr[2..3], daddr[0..1]
-        const uint32_t d8 = mine[((2u ^ rsw) << 2) | 0u];   // bytes 32..35
-        const uint32_t ihl = (d3 >> 16) & 0xfu;
-        const uint32_t ihl4 = ihl << 2;
-
-        // toeplitz_dispatch's checks (ff_dpdk_if.c:1956-1986)
-        const uint32_t et = ((d3 & 0xffu) << 8) | ((d3 >> 8) & 0xffu);
-        int qv = YRSS_DEFAULT_Q;
-        bool hashed = false;
-        if (valid && L >= 14u) {
-            if (et == 0x0800u) {
-                const uint32_t ip_len = L - 14u;
-                hashed = ip_len >= 20u && ip_len >= ihl4 && (L - ihl4) >= 20u &&
-                         (d5 >> 24) == 6u;
-            } else if (et == 0x0806u || et == 0x8035u) {
-                qv = 0;
-            }
-        }
-        uint32_t h = 0;
-        if (hashed) {
-            // TCP ports at p = 14 + 4*IHL: dwords 3+IHL (bytes 2,3) and 4+IHL (0,1).
-            const uint32_t j = 3u + ihl;
-            uint32_t pa, pb;
-            bool trunc = false;
-            if (j + 1u < 16u) {
-                pa = mine[(((j >> 2) ^ rsw) << 2) | (j & 3u)];
-                pb = mine[((((j + 1u) >> 2) ^ rsw) << 2) | ((j + 1u) & 3u)];
-            } else if (18u + ihl4 <= P.stride) {
-                const uint32_t *g = reinterpret_cast<const uint32_t *>(
-                    P.win + (size_t)pkt * P.stride);
-                pa = g[j];
-                pb = g[j + 1u];
-            } else {
-                pa = pb = 0u;
-                trunc = true;
-            }
-            // Tuple = LE image of ntohl(src), ntohl(dst), ntohs(sport), ntohs(dport)
-            // (ff_dpdk_if.c:1994-2021).
-            h = tbl[0 * 256 + ((d7 >> 8) & 0xffu)] ^     // b29
-                tbl[1 * 256 + (d7 & 0xffu)] ^            // b28
-                tbl[2 * 256 + (d6 >> 24)] ^              // b27
-                tbl[3 * 256 + ((d6 >> 16) & 0xffu)] ^    // b26
-                tbl[4 * 256 + ((d8 >> 8) & 0xffu)] ^     // b33
-                tbl[5 * 256 + (d8 & 0xffu)] ^            // b32
-                tbl[6 * 256 + (d7 >> 24)] ^              // b31
-                tbl[7 * 256 + ((d7 >> 16) & 0xffu)] ^    // b30
-                tbl[8 * 256 + (pa >> 24)] ^              // b[p+1]
-                tbl[9 * 256 + ((pa >> 16) & 0xffu)] ^    // b[p]
-                tbl[10 * 256 + ((pb >> 8) & 0xffu)] ^    // b[p+3]
-                tbl[11 * 256 + (pb & 0xffu)];            // b[p+2]
-            // hash % d exactly (Lemire fastmod, 64-bit M), then +q_off (:2031-2034)
-            const uint64_t low = P.mod_m * (uint64_t)h;
-            const uint32_t rem = (uint32_t)__umul64hi(low, (uint64_t)P.mod_d);
-            qv = (int)(uint16_t)(rem + P.q_off);
-            if (trunc) {
-                qv = YRSS_Q_TRUNCATED;
-                h = 0u;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-
-        if (valid) {
-            P.q[pkt] = (int16_t)qv;
-            if (P.hash)
-                P.hash[pkt] = h;
-        }
-
-        if (kCount) {
-            const uint32_t bkt = bucket_of(qv, P.nq);
-            uint64_t pending = __ballot(valid);
-            while (pending) {
-                const int leader = __builtin_ctzll(pending);
-                const uint32_t B = __builtin_amdgcn_readlane(bkt, leader);
-                const uint64_t m = __ballot(valid && bkt == B);
-                if (lane == 0)
-                    cnt[B] += (uint32_t)__popcll(m);
-                pending &= ~m;
-            }
+        for (int u = 0; u < kUnroll; ++u) {
+            const uint32_t tu = t0 + u * kTile;
+            if (u == 0 || tu < end)
+                process_tile<kCount>(P, tbl, stage, cnt, tu, end, lane, r[u], L[u]);
         }
     }
 
@@ -306,13 +359,13 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(const uint32_t *seg_
 // ---------------------------------------------------------------------------
 // Kernel 3: stable scatter of packet indices into per-bucket lists.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kParseBlock) void yrss_scatter(ScatterParams P)
+__global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t wave = threadIdx.x / kWave;
     const uint32_t lane = lane_id();
     uint32_t *off = reinterpret_cast<uint32_t *>(smem) + wave * P.nb;
-    const uint32_t gw = blockIdx.x * kParseWaves + wave;
+    const uint32_t gw = blockIdx.x * kScatterWaves + wave;
 
     // start[b] = exclusive scan of totals; off[b] = start[b] + seg_off[gw][b]
     uint32_t carry = 0;
@@ -435,7 +488,14 @@ struct yrss_ctx {
     yrss_config cfg;
     int device = 0;
     int cus = 0;
-    uint32_t blocks_per_cu = 4;
+    // parse-kernel launch shape (env overrides for tuning sweeps)
+    // defaults = best of the launch-shape sweep (profiles/r01_sweep_*.json):
+    // non-temporal window loads are worth ~25%; 16 waves/CU of 512-thread
+    // workgroups keep ~64 KiB of loads in flight per CU.
+    uint32_t parse_block = 512;  // YRSS_BLOCK: 256 / 512 / 1024
+    uint32_t unroll = 1;         // YRSS_UNROLL: 1 / 2
+    bool nt = true;              // YRSS_NT
+    uint32_t waves_per_cu = 16;  // YRSS_WAVES_PER_CU: cap on resident waves
     uint32_t nb = 0;
     ParseParams proto{};        // key schedule, modulo constants
     // compaction workspace, sized for the grid cap
@@ -481,20 +541,56 @@ int hip_fail(const char *what, hipError_t e)
             return hip_fail(#call, e_);                  \
     } while (0)
 
+size_t parse_lds(const yrss_ctx *c)
+{
+    const size_t w = c->parse_block / kWave;
+    return kTblBytes + w * kStageBytes + w * c->nb * sizeof(uint32_t);
+}
+
 uint32_t grid_for(const yrss_ctx *c, uint32_t n)
 {
-    const uint32_t per_block = kParseWaves * kTile;
+    const uint32_t wpb = c->parse_block / kWave;
+    const uint32_t per_block = wpb * kTile;
     const uint32_t want = (n + per_block - 1) / per_block;
-    const uint32_t cap = (uint32_t)c->cus * c->blocks_per_cu;
+    const uint32_t by_lds = (uint32_t)(160u * 1024u / parse_lds(c));
+    const uint32_t by_waves = std::max(1u, c->waves_per_cu / wpb);
+    const uint32_t cap = (uint32_t)c->cus * std::max(1u, std::min(by_lds, by_waves));
     return std::max(1u, std::min(want, cap));
 }
 
-uint32_t seg_for(uint32_t n, uint32_t grid)
+uint32_t seg_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
 {
-    const uint32_t waves = grid * kParseWaves;
+    const uint32_t waves = grid * (c->parse_block / kWave);
     uint32_t s = (n + waves - 1) / waves;
     s = (s + kTile - 1) / kTile * kTile;
     return std::max<uint32_t>(s, kTile);
+}
+
+typedef void (*ParseKernel)(ParseParams);
+
+template <bool C, int U, bool NT>
+ParseKernel pick_block(uint32_t block)
+{
+    switch (block) {
+    case 256: return yrss_parse_hash<C, U, NT, 256>;
+    case 1024: return yrss_parse_hash<C, U, NT, 1024>;
+    default: return yrss_parse_hash<C, U, NT, 512>;
+    }
+}
+
+ParseKernel pick_parse(const yrss_ctx *c, bool compact)
+{
+    const int v = (compact ? 4 : 0) | (c->unroll == 2 ? 2 : 0) | (c->nt ? 1 : 0);
+    switch (v) {
+    case 0: return pick_block<false, 1, false>(c->parse_block);
+    case 1: return pick_block<false, 1, true>(c->parse_block);
+    case 2: return pick_block<false, 2, false>(c->parse_block);
+    case 3: return pick_block<false, 2, true>(c->parse_block);
+    case 4: return pick_block<true, 1, false>(c->parse_block);
+    case 5: return pick_block<true, 1, true>(c->parse_block);
+    case 6: return pick_block<true, 2, false>(c->parse_block);
+    default: return pick_block<true, 2, true>(c->parse_block);
+    }
 }
 
 hipEvent_t take_event(yrss_ctx *c)
@@ -663,10 +759,19 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     c->cfg = *cfg;
     c->device = cfg->device;
     c->cus = prop.multiProcessorCount;
-    if (const char *e = getenv("YRSS_BLOCKS_PER_CU")) {
+    if (const char *e = getenv("YRSS_BLOCK")) {
         const int v = atoi(e);
-        if (v >= 1 && v <= 16)
-            c->blocks_per_cu = (uint32_t)v;
+        if (v == 256 || v == 512 || v == 1024)
+            c->parse_block = (uint32_t)v;
+    }
+    if (const char *e = getenv("YRSS_UNROLL"))
+        c->unroll = atoi(e) == 1 ? 1u : 2u;
+    if (const char *e = getenv("YRSS_NT"))
+        c->nt = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_WAVES_PER_CU")) {
+        const int v = atoi(e);
+        if (v >= 4 && v <= kMaxWavesPerCU)
+            c->waves_per_cu = (uint32_t)v;
     }
     c->nb = (uint32_t)cfg->nb_queues + 1u;
     compute_key_schedule(cfg, c->proto.kwin);
@@ -677,7 +782,7 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     c->proto.nq = cfg->nb_queues;
     c->proto.nb = c->nb;
 
-    c->seg_cap = (uint32_t)c->cus * c->blocks_per_cu * kParseWaves;
+    c->seg_cap = (uint32_t)c->cus * kMaxWavesPerCU;   // >= grid * waves per block
     const size_t ws = (size_t)c->seg_cap * c->nb * sizeof(uint32_t);
     hipError_t e;
     if ((e = hipMalloc((void **)&c->d_seg_cnt, ws)) != hipSuccess ||
@@ -743,8 +848,8 @@ int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
     }
 
     const uint32_t grid = grid_for(c, n);
-    const uint32_t seg = seg_for(n, grid);
-    const uint32_t nseg = grid * kParseWaves;
+    const uint32_t seg = seg_for(c, n, grid);
+    const uint32_t nseg = grid * (c->parse_block / kWave);   // multiple of kScatterWaves
 
     ParseParams P = c->proto;
     P.win = d_win;
@@ -755,14 +860,10 @@ int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
     P.n = n;
     P.stride = win_stride;
     P.seg = seg;
-    const size_t lds = kTblBytes + kParseWaves * kStageBytes +
-                       (size_t)kParseWaves * c->nb * sizeof(uint32_t);
     {
         Timed t(c, s, YRSS_K_PARSE_HASH);
-        if (compact)
-            hipLaunchKernelGGL(yrss_parse_hash<true>, dim3(grid), dim3(kParseBlock), lds, s, P);
-        else
-            hipLaunchKernelGGL(yrss_parse_hash<false>, dim3(grid), dim3(kParseBlock), lds, s, P);
+        hipLaunchKernelGGL(pick_parse(c, compact), dim3(grid), dim3(c->parse_block),
+                           parse_lds(c), s, P);
     }
     YRSS_HIP(hipGetLastError());
     if (!compact)
@@ -786,8 +887,8 @@ int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
     S.nb = c->nb;
     {
         Timed t(c, s, YRSS_K_SCATTER);
-        hipLaunchKernelGGL(yrss_scatter, dim3(grid), dim3(kParseBlock),
-                           (size_t)kParseWaves * c->nb * sizeof(uint32_t), s, S);
+        hipLaunchKernelGGL(yrss_scatter, dim3(nseg / kScatterWaves), dim3(kScatterBlock),
+                           (size_t)kScatterWaves * c->nb * sizeof(uint32_t), s, S);
     }
     YRSS_HIP(hipGetLastError());
     return 0;
