@@ -140,6 +140,34 @@ def cpu_baseline(args, nb_queues):
     }
 
 
+def probe_traffic(win, lens, out, n, stride, steps):
+    """Average duration of the ideal-traffic twin (tools/yrss_probe.hip) over
+    the same buffers: the practical floor of the parse kernel on this box."""
+    import ctypes
+
+    import torch
+
+    lib_path = ROOT / "tools" / "libyrss_probe.so"
+    if stride != 64 or not lib_path.exists():
+        return None
+    lib = ctypes.CDLL(str(lib_path))
+    fn = lib.yrss_probe_traffic_launch
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32, ctypes.c_void_p]
+    stream = torch.cuda.current_stream()
+    args = (win.data_ptr(), lens.data_ptr(), out.q.data_ptr(), out.hash.data_ptr(), n,
+            stream.cuda_stream)
+    for _ in range(3):
+        fn(*args)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(steps):
+        fn(*args)
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / steps / 1e3
+
+
 def load_traffic(path: str, key: dict):
     """Per-launch HBM bytes for the parse kernel from a committed PMC summary
     of the same workload (profiles/pmc_parse_hash.json), else None."""
@@ -176,6 +204,7 @@ def main(argv=None):
     def step():
         eng.dispatch_dev(win, lens, args.stride, n, out=out, compact=not args.no_compact)
 
+    probe_s = probe_traffic(win, lens, out, n, args.stride, max(args.steps, 10))
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -254,6 +283,11 @@ def main(argv=None):
                 "traffic": traffic,
                 "kernel": "yrss_parse_hash", "bytes_per_pkt": bpp,
                 "kernel_avg_us": round(k_avg_s * 1e6, 2),
+                "probe": None if probe_s is None else {
+                    "what": "ideal-traffic twin (tools/yrss_probe.hip): same bytes, no parse",
+                    "us": round(probe_s * 1e6, 2),
+                    "achieved": round(bpp * n / probe_s / 1e9, 1),
+                    "parse_frac_of_probe": round(probe_s / k_avg_s, 4)},
             },
             "cpu_baseline": cpu,
             "check": check,

@@ -55,7 +55,7 @@ struct ParseParams {
     const uint16_t *len;
     int16_t *q;
     uint32_t *hash;       // may be null
-    uint32_t *seg_cnt;    // [segments][nb] or null (no compaction)
+    uint32_t *seg_cnt;    // [nb][nseg] bucket-major, or null (no compaction)
     uint32_t n;
     uint32_t stride;
     uint32_t seg;         // packets per wave segment, multiple of kTile
@@ -63,14 +63,14 @@ struct ParseParams {
     uint32_t nb;          // buckets = nq + 1 (last = drop)
     uint32_t mod_d;       // divisor: nb_procs or nb_procs-1
     uint32_t q_off;       // 0 or 1 (dispatch_only_core)
-    uint32_t pad_;
+    uint32_t nseg;        // wave segments in this launch
     uint64_t mod_m;       // Lemire fastmod constant for mod_d
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
 struct ScatterParams {
     const int16_t *q;
-    const uint32_t *seg_off;   // [segments][nb] exclusive per-bucket scan
+    const uint32_t *seg_off;   // [nb][nseg] exclusive per-bucket scan
     const uint32_t *totals;    // [nb]
     uint32_t *qidx;
     uint32_t *qstart;          // [nb + 1]
@@ -78,6 +78,7 @@ struct ScatterParams {
     uint32_t seg;
     uint32_t nq;
     uint32_t nb;
+    uint32_t nseg;
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -220,7 +221,7 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
     if (valid) {
         P.q[pkt] = (int16_t)qv;
         if (P.hash)
-            P.hash[pkt] = h;
+            __builtin_nontemporal_store(h, P.hash + pkt);   // never re-read here
     }
 
     if (kCount) {
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (uint32_t b = lane; b < P.nb; b += kWave)
-            P.seg_cnt[(size_t)gw * P.nb + b] = cnt[b];
+            P.seg_cnt[(size_t)b * P.nseg + gw] = cnt[b];
     }
 }
 
@@ -309,6 +310,19 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
 // ---------------------------------------------------------------------------
 constexpr int kScanBlock = 1024;
 
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
+{
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, kWave);
+        if (lane >= (uint32_t)d)
+            x += y;
+    }
+    return x;
+}
+
+// seg_cnt/seg_off are bucket-major ([nb][nseg]) so one workgroup scans one
+// contiguous row with 16-byte loads; nseg is a multiple of 8.
 __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(const uint32_t *seg_cnt,
                                                             uint32_t *seg_off,
                                                             uint32_t *totals,
@@ -316,41 +330,42 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(const uint32_t *seg_
 {
     __shared__ uint32_t wsum[kScanBlock / kWave];
     const uint32_t b = blockIdx.x;
-    const uint32_t per = (nseg + kScanBlock - 1) / kScanBlock;
-    const uint32_t s0 = threadIdx.x * per;
+    const uint32_t lane = lane_id(), wave = threadIdx.x / kWave;
+    const uint32_t nvec = nseg / 4u;                       // uint4 per row
+    const uint32_t per = (nvec + kScanBlock - 1) / kScanBlock;
+    const uint4 *row = reinterpret_cast<const uint4 *>(seg_cnt + (size_t)b * nseg);
+    uint4 *orow = reinterpret_cast<uint4 *>(seg_off + (size_t)b * nseg);
+    uint4 v[2];
     uint32_t local = 0;
-    for (uint32_t s = s0; s < s0 + per && s < nseg; ++s)
-        local += seg_cnt[(size_t)s * nb + b];
-    // inclusive wave scan
-    uint32_t x = local;
-    const uint32_t lane = lane_id();
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, kWave);
-        if (lane >= (uint32_t)d)
-            x += y;
+    for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t i = threadIdx.x * per + k;
+        v[k] = (k < per && i < nvec) ? row[i] : make_uint4(0u, 0u, 0u, 0u);
+        local += v[k].x + v[k].y + v[k].z + v[k].w;
     }
-    const uint32_t wave = threadIdx.x / kWave;
+    const uint32_t x = wave_incl_scan(local, lane);
     if (lane == kWave - 1)
         wsum[wave] = x;
     __syncthreads();
     if (wave == 0) {
-        uint32_t v = lane < kScanBlock / kWave ? wsum[lane] : 0u;
-#pragma unroll
-        for (int d = 1; d < kScanBlock / kWave; d <<= 1) {
-            const uint32_t y = __shfl_up(v, d, kWave);
-            if (lane >= (uint32_t)d)
-                v += y;
-        }
+        const uint32_t w = lane < kScanBlock / kWave ? wsum[lane] : 0u;
+        const uint32_t ws = wave_incl_scan(w, lane);
         if (lane < kScanBlock / kWave)
-            wsum[lane] = v;
+            wsum[lane] = ws;
     }
     __syncthreads();
     uint32_t run = x - local + (wave ? wsum[wave - 1] : 0u);
-    for (uint32_t s = s0; s < s0 + per && s < nseg; ++s) {
-        const uint32_t c = seg_cnt[(size_t)s * nb + b];
-        seg_off[(size_t)s * nb + b] = run;
-        run += c;
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t i = threadIdx.x * per + k;
+        if (k < per && i < nvec) {
+            uint4 o;
+            o.x = run; run += v[k].x;
+            o.y = run; run += v[k].y;
+            o.z = run; run += v[k].z;
+            o.w = run; run += v[k].w;
+            orow[i] = o;
+        }
     }
     if (threadIdx.x == kScanBlock - 1)
         totals[b] = run;
@@ -381,7 +396,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
         }
         const uint32_t start = carry + x - t;
         if (b < P.nb) {
-            off[b] = start + P.seg_off[(size_t)gw * P.nb + b];
+            off[b] = start + P.seg_off[(size_t)b * P.nseg + gw];
             if (gw == 0)
                 P.qstart[b] = start;
         }
@@ -403,7 +418,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
 #pragma unroll
         for (int j = 0; j < kScatterRound; ++j) {
             const uint32_t pkt = r0 + j * kWave + lane;
-            bk[j] = bucket_of(P.q[min(pkt, end - 1u)], P.nq);
+            bk[j] = bucket_of(__builtin_nontemporal_load(P.q + min(pkt, end - 1u)), P.nq);
             pend |= (pkt < end ? 1u : 0u) << j;
         }
         for (;;) {
@@ -423,7 +438,8 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
                 const bool take = ((pend >> j) & 1u) && bk[j] == B;
                 const uint64_t m = __ballot(take);
                 if (take)
-                    P.qidx[base + run + rank_below(m)] = r0 + j * kWave + lane;
+                    __builtin_nontemporal_store(r0 + j * kWave + lane,
+                                                P.qidx + base + run + rank_below(m));
                 run += (uint32_t)__popcll(m);
                 pend &= ~((take ? 1u : 0u) << j);
             }
@@ -860,6 +876,7 @@ int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
     P.n = n;
     P.stride = win_stride;
     P.seg = seg;
+    P.nseg = nseg;
     {
         Timed t(c, s, YRSS_K_PARSE_HASH);
         hipLaunchKernelGGL(pick_parse(c, compact), dim3(grid), dim3(c->parse_block),
@@ -885,6 +902,7 @@ int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
     S.seg = seg;
     S.nq = c->cfg.nb_queues;
     S.nb = c->nb;
+    S.nseg = nseg;
     {
         Timed t(c, s, YRSS_K_SCATTER);
         hipLaunchKernelGGL(yrss_scatter, dim3(nseg / kScatterWaves), dim3(kScatterBlock),
