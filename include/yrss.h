@@ -148,6 +148,41 @@ int yrss_dispatch_dev(yrss_ctx *ctx, const uint8_t *d_win, uint32_t win_stride,
                       uint32_t *d_hash, uint32_t *d_qidx, uint32_t *d_qstart,
                       void *stream);
 
+/* ---- protocol_filter / KNI ----------------------------- */
+
+/* Per-packet protocol_filter class (fs/lib/ff_dpdk_kni.h:34-38 FilterReturn),
+ * computed in the same kernel pass as the hash when requested. */
+#define YRSS_FILTER_UNKNOWN (-1)
+#define YRSS_FILTER_ARP 1
+#define YRSS_FILTER_KNI 2
+/* Boundary outcomes the reference cannot produce: the IPIP header walk left
+ * the staged window, or hit IHL=0 under IPIP, where ff_kni_proto_filter
+ * recurses on the same header forever (ff_dpdk_kni.c:274-275). */
+#define YRSS_FILTER_TRUNC (-2)
+#define YRSS_FILTER_LOOP (-3)
+
+/* Configure KNI exactly as ff_kni_init/init_kni do (ff_dpdk_if.c:597-606,
+ * ff_dpdk_kni.c:99-118,300-331): enable, method "accept"/"reject" (anything
+ * else is rejected like ff_config.c:548-553), and comma/range port lists
+ * ("80,443,8000-8080") parsed with kni_set_bitmap's rules into the 8 KiB
+ * htons-indexed bitmaps.  NULL lists leave a bitmap empty. */
+int yrss_set_kni(yrss_ctx *ctx, int enable, const char *method,
+                 const char *tcp_ports, const char *udp_ports);
+
+/* Full device batch: yrss_dispatch_dev plus the optional filter output. */
+struct yrss_dev_batch {
+    const uint8_t *win;       /* as d_win of yrss_dispatch_dev          */
+    uint32_t win_stride;
+    uint32_t n;
+    const uint16_t *len;
+    int16_t *q;
+    uint32_t *hash;           /* may be NULL                            */
+    uint32_t *qidx;           /* may be NULL                            */
+    uint32_t *qstart;         /* required with qidx                     */
+    int8_t *filter;           /* YRSS_FILTER_* per packet, or NULL      */
+};
+int yrss_dispatch_dev_ex(yrss_ctx *ctx, const struct yrss_dev_batch *b, void *stream);
+
 /* ---- host-resident dispatch (the drop-in burst hook) ------------------------ */
 
 /* Classify a burst of DPDK mbufs straight off rte_eth_rx_burst.
@@ -168,6 +203,46 @@ int yrss_dispatch_frames(yrss_ctx *ctx, const uint8_t *const *data,
                          const uint16_t *len, uint32_t n, int16_t *out_q,
                          uint32_t *out_hash, uint32_t *out_qidx,
                          uint32_t *out_qstart);
+
+/* ---- burst routing: process_packets' hand-off --------- */
+
+/* Caller-side plumbing, so the routing drives real DPDK objects:
+ *   enqueue  rte_ring_enqueue_burst(dispatch_ring[port][queue], objs, n) —
+ *            returns how many of objs (a prefix) were enqueued
+ *   clone    pktmbuf_deep_clone(m, pool of queue) (ff_dpdk_if.c:1009-1056);
+ *            NULL when the pool is exhausted
+ *   release  rte_pktmbuf_free(m) */
+struct yrss_route_ops {
+    unsigned (*enqueue)(void *user, uint16_t queue, void *const *objs, unsigned n);
+    void *(*clone)(void *user, void *mbuf, uint16_t queue);
+    void (*release)(void *user, void *mbuf);
+    void *user;
+};
+
+struct yrss_route_result {
+    uint32_t n_local;         /* out_local[]: ff_veth_input on this lcore, in order */
+    uint32_t n_kni;           /* out_kni[]: ff_kni_enqueue, in order                */
+    uint32_t n_freed;         /* bad queue, ring full or failed clone enqueue       */
+    uint32_t n_arp;           /* ARP packets kept local (and cloned)               */
+    uint32_t n_unresolved;    /* YRSS_FILTER_TRUNC/LOOP packets, left in out_local */
+    uint32_t n_ring[YRSS_MAX_QUEUES];   /* objects enqueued per queue ring        */
+};
+
+/* process_packets(port, queue_id, mbufs, n, ctx, pkts_from_ring=0) with the
+ * dispatcher registered (ff_dpdk_if.c:1058-1140), for a whole burst: classify
+ * on the GPU (queue + protocol_filter), then per packet in order
+ *   ret < 0 || ret >= nb_queues        -> release (:1080-1083)
+ *   ret != queue_id                    -> ring[ret], FIFO; release if full (:1087-1093)
+ *   local, FILTER_ARP                  -> clone to every other queue's ring, a KNI
+ *                                         clone if KNI is on and kni_primary, and
+ *                                         local input (:1097-1129)
+ *   local, KNI accept/reject rule      -> out_kni (:1132-1135)
+ *   local, otherwise                   -> out_local (:1137)
+ * Ring order equals the reference's one-at-a-time enqueue order.  out_local and
+ * out_kni need room for n (+ n ARP clones for out_kni). */
+int yrss_route_burst(yrss_ctx *ctx, void *const *mbufs, uint32_t n, uint16_t queue_id,
+                     int kni_primary, const struct yrss_route_ops *ops, void **out_local,
+                     void **out_kni, struct yrss_route_result *res);
 
 /* ---- synthetic traffic (bench / parity inputs; see yrss_synth.h) ------------- */
 

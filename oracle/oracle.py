@@ -70,6 +70,13 @@ def lib() -> ctypes.CDLL:
                                           ctypes.c_uint16, ctypes.c_uint16]
         L.oracle_synth.restype = None
         L.oracle_synth.argtypes = [ctypes.POINTER(SynthParams), ctypes.c_uint64, u32, vp, u32, vp]
+        L.oracle_kni_set_bitmap.restype = None
+        L.oracle_kni_set_bitmap.argtypes = [ctypes.c_char_p, vp]
+        L.oracle_protocol_filter.restype = ctypes.c_int
+        L.oracle_protocol_filter.argtypes = [ctypes.c_char_p, ctypes.c_uint16, u32, ctypes.c_int,
+                                             vp, vp]
+        L.oracle_filter_windows.restype = None
+        L.oracle_filter_windows.argtypes = [vp, u32, vp, u32, ctypes.c_int, vp, vp, vp]
         L.oracle_bench_dispatch.restype = ctypes.c_uint64
         L.oracle_bench_dispatch.argtypes = [vp, u32, vp, u32, ctypes.POINTER(OracleCfg), u32,
                                             ctypes.c_int]
@@ -147,3 +154,70 @@ def bench_dispatch(win, stride, lens, c: OracleCfg, reps: int, fast: bool = Fals
     lens = np.ascontiguousarray(lens).view(np.uint16)
     return lib().oracle_bench_dispatch(win.ctypes.data, stride, lens.ctypes.data, int(lens.size),
                                        ctypes.byref(c), reps, 1 if fast else 0)
+
+
+def kni_bitmap(ports: str | None) -> np.ndarray:
+    bm = np.zeros(8192, np.uint8)
+    lib().oracle_kni_set_bitmap(None if ports is None else ports.encode(), bm.ctypes.data)
+    return bm
+
+
+def protocol_filter(frame: bytes, length: int, enable_kni: bool, tcp_bm, udp_bm,
+                    avail: int = 1 << 20) -> int:
+    buf = bytes(frame) + bytes(max(0, 80 - len(frame)))
+    return lib().oracle_protocol_filter(buf, length, min(avail, len(buf)), 1 if enable_kni else 0,
+                                        tcp_bm.ctypes.data, udp_bm.ctypes.data)
+
+
+def filter_windows(win, stride, lens, enable_kni, tcp_bm, udp_bm) -> np.ndarray:
+    n = int(lens.size)
+    win = np.ascontiguousarray(win, dtype=np.uint8)
+    lens = np.ascontiguousarray(lens).view(np.uint16)
+    out = np.empty(max(n, 1), np.int8)
+    lib().oracle_filter_windows(win.ctypes.data, stride, lens.ctypes.data, n,
+                                1 if enable_kni else 0, tcp_bm.ctypes.data, udp_bm.ctypes.data,
+                                out.ctypes.data)
+    return out[:n]
+
+
+def process_packets_route(q, fclass, nb_queues, queue_id, kni_enable, kni_accept, kni_primary,
+                          ring_free, clone_ok=lambda i, j: True):
+    """Pure-Python restatement of process_packets (ff_dpdk_if.c:1058-1140) for
+    a burst from the NIC (pkts_from_ring = 0), one packet at a time, small
+    bursts only.  ring_free[j] = free slots of dispatch_ring[port][j].
+    Returns (rings: {j: [obj]}, local: [obj], kni: [obj], freed: [obj]) where
+    obj = ("pkt", i) or ("clone", i, j)."""
+    rings = {j: [] for j in range(nb_queues)}
+    local, kni, freed = [], [], []
+    free = list(ring_free)
+    for i, ret in enumerate(q):
+        ret = int(ret)
+        if ret < 0 or ret >= nb_queues:
+            freed.append(("pkt", i))
+            continue
+        if ret != queue_id:
+            if free[ret] > 0:
+                rings[ret].append(("pkt", i))
+                free[ret] -= 1
+            else:
+                freed.append(("pkt", i))
+            continue
+        f = int(fclass[i])
+        if f == 1:                                   # FILTER_ARP
+            for j in range(nb_queues):
+                if j == queue_id:
+                    continue
+                if clone_ok(i, j):
+                    if free[j] > 0:
+                        rings[j].append(("clone", i, j))
+                        free[j] -= 1
+                    else:
+                        freed.append(("clone", i, j))
+            if kni_enable and kni_primary and clone_ok(i, 0xFFFF):
+                kni.append(("clone", i, 0xFFFF))
+            local.append(("pkt", i))
+        elif kni_enable and ((f == 2 and kni_accept) or (f == -1 and not kni_accept)):
+            kni.append(("pkt", i))
+        else:
+            local.append(("pkt", i))
+    return rings, local, kni, freed

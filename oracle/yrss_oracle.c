@@ -22,9 +22,12 @@
  *   toeplitz_dispatch    fs/lib/ff_dpdk_if.c:1945-2113
  *   process_packets      fs/lib/ff_dpdk_if.c:1058-1094 (dispatcher block)
  *   ff_rss_check         fs/lib/ff_dpdk_if.c:1904-1940
+ *   protocol_filter      fs/lib/ff_dpdk_if.c:976-996, ff_dpdk_kni.c:218-290
+ *   kni_set_bitmap       fs/lib/ff_dpdk_kni.c:84-118
  */
 #include <stddef.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../include/yrss_synth.h"
@@ -275,4 +278,97 @@ uint64_t oracle_bench_dispatch(const uint8_t *win, uint32_t stride, const uint16
             sum += (uint64_t)q * 0x9E3779B97F4A7C15ull + h;
         }
     return sum;
+}
+
+/* ---- protocol_filter / KNI ---------------------------------- */
+
+/* kni_set_bitmap (ff_dpdk_kni.c:99-118) with set_bitmap (:84-89): a '-' found
+ * before the next ',' (at least one char between) makes an atoi range; each
+ * value is truncated to uint16_t and stored at bit 0x80 >> (p % 8) of byte
+ * p / 8 where p = htons(port). */
+static void set_port(uint8_t *bm, uint16_t port)
+{
+    const uint16_t p = (uint16_t)((port >> 8) | (port << 8));
+    bm[p / 8] |= (uint8_t)(0x80 >> (p % 8));
+}
+
+void oracle_kni_set_bitmap(const char *s, uint8_t *bm)
+{
+    if (!s)
+        return;
+    const char *head = s;
+    for (;;) {
+        const char *comma = strstr(head, ",");
+        const char *dash = strstr(head, "-");
+        if (dash && (!comma || dash < comma - 1)) {
+            long count = 0;
+            for (long v = atol(head); v <= atol(dash + 1) && count < 65536; ++v, ++count)
+                set_port(bm, (uint16_t)v);
+        } else {
+            set_port(bm, (uint16_t)atol(head));
+        }
+        if (!comma)
+            break;
+        head = comma + 1;
+    }
+}
+
+static int port_in(const uint8_t *bm, uint16_t raw)
+{
+    return (bm[raw / 8] & (0x80 >> (raw % 8))) != 0;
+}
+
+/* protocol_filter (ff_dpdk_if.c:976-996) + ff_kni_proto_filter /
+ * protocol_filter_ip/_tcp/_udp (ff_dpdk_kni.c:218-290).  `avail` is how many
+ * bytes of the frame are readable (the staged window); a header walk that
+ * needs more returns -2 (TRUNC).  IHL=0 under IPIP makes the reference recurse
+ * on the same header forever: returned as -3 (LOOP) instead of hanging. */
+int oracle_protocol_filter(const uint8_t *b, uint16_t len, uint32_t avail, int enable_kni,
+                           const uint8_t *tcp_bm, const uint8_t *udp_bm)
+{
+    if (len < 14)
+        return -1;                                    /* FILTER_UNKNOWN */
+    const unsigned et = ((unsigned)b[12] << 8) | b[13];
+    if (et == 0x0806)
+        return 1;                                     /* FILTER_ARP */
+    if (!enable_kni || et != 0x0800)
+        return -1;
+    uint32_t o = 14, left = (uint16_t)(len - 14);
+    for (;;) {                                        /* protocol_filter_ip */
+        if (left < 20)
+            return -1;
+        if (o >= avail)
+            return -2;
+        const uint32_t hl = (b[o] & 0x0f) << 2;
+        if (left < hl)
+            return -1;
+        if (o + 9 >= avail)
+            return -2;
+        const unsigned pr = b[o + 9];
+        const uint32_t nx = o + hl;
+        const uint16_t nl = (uint16_t)(left - hl);
+        if (pr == 6 || pr == 17) {                    /* _tcp: len>=20, _udp: len>=8 */
+            if (nl < (pr == 6 ? 20 : 8))
+                return -1;
+            if (nx + 3 >= avail)
+                return -2;
+            const uint16_t raw = (uint16_t)(b[nx + 2] | (b[nx + 3] << 8));  /* hdr->dst_port */
+            return port_in(pr == 6 ? tcp_bm : udp_bm, raw) ? 2 : -1;
+        }
+        if (pr != 4)                                  /* IPPROTO_IPIP recurses */
+            return -1;
+        if (hl == 0)
+            return -3;
+        o = nx;
+        left = nl;
+    }
+}
+
+void oracle_filter_windows(const uint8_t *win, uint32_t stride, const uint16_t *len, uint32_t n,
+                           int enable_kni, const uint8_t *tcp_bm, const uint8_t *udp_bm,
+                           int8_t *out)
+{
+    for (uint32_t i = 0; i < n; ++i)
+        out[i] = (int8_t)oracle_protocol_filter(win + (size_t)i * stride, len[i], stride,
+                                                enable_kni, tcp_bm, udp_bm);
 }

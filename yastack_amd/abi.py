@@ -30,6 +30,10 @@ F_WRITE_RSS = 0x1
 
 K_PARSE_HASH, K_SCAN, K_SCATTER = 0, 1, 2
 
+# protocol_filter classes (ff_dpdk_kni.h:34-38) + boundary outcomes
+FILTER_UNKNOWN, FILTER_ARP, FILTER_KNI, FILTER_TRUNC, FILTER_LOOP = -1, 1, 2, -2, -3
+ROUTE_KNI_QUEUE = 0xFFFF   # queue argument of the clone callback for the KNI clone
+
 # struct rte_mbuf offsets of DPDK 18.02 (dpdk/lib/librte_mbuf/rte_mbuf.h:412-560)
 MBUF_OFF_BUF_ADDR = 0
 MBUF_OFF_DATA_OFF = 16
@@ -76,6 +80,46 @@ class Config(ctypes.Structure):
     ]
 
 
+class DevBatch(ctypes.Structure):
+    _fields_ = [
+        ("win", ctypes.c_void_p),
+        ("win_stride", ctypes.c_uint32),
+        ("n", ctypes.c_uint32),
+        ("len", ctypes.c_void_p),
+        ("q", ctypes.c_void_p),
+        ("hash", ctypes.c_void_p),
+        ("qidx", ctypes.c_void_p),
+        ("qstart", ctypes.c_void_p),
+        ("filter", ctypes.c_void_p),
+    ]
+
+
+ENQUEUE_FN = ctypes.CFUNCTYPE(ctypes.c_uint, ctypes.c_void_p, ctypes.c_uint16,
+                              ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint)
+CLONE_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint16)
+RELEASE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+
+
+class RouteOps(ctypes.Structure):
+    _fields_ = [
+        ("enqueue", ENQUEUE_FN),
+        ("clone", CLONE_FN),
+        ("release", RELEASE_FN),
+        ("user", ctypes.c_void_p),
+    ]
+
+
+class RouteResult(ctypes.Structure):
+    _fields_ = [
+        ("n_local", ctypes.c_uint32),
+        ("n_kni", ctypes.c_uint32),
+        ("n_freed", ctypes.c_uint32),
+        ("n_arp", ctypes.c_uint32),
+        ("n_unresolved", ctypes.c_uint32),
+        ("n_ring", ctypes.c_uint32 * MAX_QUEUES),
+    ]
+
+
 class SynthParams(ctypes.Structure):
     _fields_ = [
         ("seed", ctypes.c_uint64),
@@ -102,6 +146,12 @@ _PROTOS = {
     "yrss_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(_u32)]),
     "yrss_grid_for": (_u32, [_vp, _u32]),
+    "yrss_set_kni": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
+                                    ctypes.c_char_p]),
+    "yrss_dispatch_dev_ex": (ctypes.c_int, [_vp, ctypes.POINTER(DevBatch), _vp]),
+    "yrss_route_burst": (ctypes.c_int, [_vp, _vp, _u32, ctypes.c_uint16, ctypes.c_int,
+                                        ctypes.POINTER(RouteOps), _vp, _vp,
+                                        ctypes.POINTER(RouteResult)]),
 }
 
 _lib = None

@@ -33,6 +33,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <strings.h>
+
 #include <vector>
 
 #include "yrss.h"
@@ -65,6 +67,10 @@ struct ParseParams {
     uint32_t q_off;       // 0 or 1 (dispatch_only_core)
     uint32_t nseg;        // wave segments in this launch
     uint64_t mod_m;       // Lemire fastmod constant for mod_d
+    int8_t *filter;       // protocol_filter class per packet, or null
+    const uint32_t *kni_bm;   // tcp bitmap (2048 words) then udp bitmap (2048 words)
+    uint32_t kni_enable;
+    uint32_t pad_;
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
@@ -95,15 +101,17 @@ __device__ __forceinline__ uint32_t bucket_of(int qv, uint32_t nq)
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 1: parse + Toeplitz hash + queue, one lane per packet.
+// Kernel 1: parse + Toeplitz hash + queue (+ protocol_filter), one lane per
+// packet.
 // ---------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kKniWords = 2 * 2048;   // two 8 KiB port bitmaps (ff_dpdk_kni.c:312-328)
 
 // One 64-packet tile's global loads: four 16-byte chunks per lane (lane l gets
 // chunk l&3 of packet t0 + 16k + l/4, i.e. 1 KiB contiguous per instruction at
 // stride 64) plus the lane's own data_len.  Addresses are clamped to the last
-// packet of the segment instead of branching, so every load always issues and
-// hipcc's vmcnt accounting stays exact across the prefetch.
+// packet of the segment instead of branching, so every load always issues.
 template <bool kNT>
 __device__ __forceinline__ void load_tile(const ParseParams &P, uint32_t t0, uint32_t end,
                                           uint32_t lane, u32x4 (&r)[4], uint32_t &L)
@@ -118,11 +126,76 @@ __device__ __forceinline__ void load_tile(const ParseParams &P, uint32_t t0, uin
     L = P.len[min(t0 + lane, end - 1u)];
 }
 
-template <bool kCount>
+// Byte k of this lane's window: from the staged LDS tile (k < 64), else from
+// HBM (k < stride, rare), else unavailable (*trunc).
+__device__ __forceinline__ uint32_t win_byte(const ParseParams &P, const uint32_t *mine,
+                                             uint32_t rsw, uint32_t pkt, uint32_t k, bool *trunc)
+{
+    if (k < 64u) {
+        const uint32_t j = k >> 2;
+        return (mine[(((j >> 2) ^ rsw) << 2) | (j & 3u)] >> (8u * (k & 3u))) & 0xffu;
+    }
+    if (k < P.stride)
+        return P.win[(size_t)pkt * P.stride + k];
+    *trunc = true;
+    return 0u;
+}
+
+// FilterReturn values (ff_dpdk_kni.h:34-38) plus the two boundary outcomes.
+constexpr int kFilterUnknown = -1, kFilterArp = 1, kFilterKni = 2;
+constexpr int kFilterTrunc = -2;   // header walk left the staged window
+constexpr int kFilterLoop = -3;    // IPIP with IHL=0: the reference recurses forever
+
+__device__ __forceinline__ int kni_port_class(const uint32_t *kni, uint32_t proto, uint32_t raw)
+{
+    // get_bitmap(hdr->dst_port): index = port as stored (network order read
+    // little-endian), bit 0x80 >> (idx % 8) of byte idx / 8 (ff_dpdk_kni.c:51-96)
+    const uint32_t base = proto == 6u ? 0u : 2048u;
+    const uint32_t byte = (kni[base + (raw >> 5)] >> (8u * ((raw >> 3) & 3u))) & 0xffu;
+    return (byte & (0x80u >> (raw & 7u))) ? kFilterKni : kFilterUnknown;
+}
+
+// Generic protocol_filter_ip walk (ff_dpdk_kni.c:255-283) from IPv4 header at
+// byte o with `left` bytes remaining, recursing through IPIP.  Rare path.
+__device__ int kni_walk(const ParseParams &P, const uint32_t *kni, const uint32_t *mine,
+                        uint32_t rsw, uint32_t pkt, uint32_t o, uint32_t left)
+{
+    bool trunc = false;
+    for (;;) {
+        if (left < 20u)
+            return kFilterUnknown;
+        const uint32_t hl = (win_byte(P, mine, rsw, pkt, o, &trunc) & 0x0fu) << 2;
+        if (trunc)
+            return kFilterTrunc;
+        if (left < hl)
+            return kFilterUnknown;
+        const uint32_t pr = win_byte(P, mine, rsw, pkt, o + 9u, &trunc);
+        if (trunc)
+            return kFilterTrunc;
+        const uint32_t nx = o + hl, nl = left - hl;
+        if (pr == 6u || pr == 17u) {
+            if (nl < (pr == 6u ? 20u : 8u))
+                return kFilterUnknown;
+            const uint32_t lo = win_byte(P, mine, rsw, pkt, nx + 2u, &trunc);
+            const uint32_t hi = win_byte(P, mine, rsw, pkt, nx + 3u, &trunc);
+            if (trunc)
+                return kFilterTrunc;
+            return kni_port_class(kni, pr, lo | (hi << 8));
+        }
+        if (pr != 4u)
+            return kFilterUnknown;
+        if (hl == 0u)
+            return kFilterLoop;
+        o = nx;
+        left = nl;
+    }
+}
+
+template <bool kCount, bool kFilter>
 __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_t *tbl,
-                                             u32x4 *stage, uint32_t *cnt, uint32_t t0,
-                                             uint32_t end, uint32_t lane, const u32x4 (&r)[4],
-                                             uint32_t Lraw)
+                                             const uint32_t *kni, u32x4 *stage, uint32_t *cnt,
+                                             uint32_t t0, uint32_t end, uint32_t lane,
+                                             const u32x4 (&r)[4], uint32_t Lraw)
 {
     // Staging layout: chunk c (16 B) of tile packet p at slot p*4 + (c ^ ((p>>2)&3)).
     // Writes: lane l holds chunk l&3 of packet 16k + l/4, so (p>>2)&3 == (l>>4)&3.
@@ -151,29 +224,26 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
     const uint32_t d8 = mine[((2u ^ rsw) << 2) | 0u];   // bytes 32..35
     const uint32_t ihl = (d3 >> 16) & 0xfu;
     const uint32_t ihl4 = ihl << 2;
+    const uint32_t proto = d5 >> 24;
+    // L4 ports at p = 14 + 4*IHL: dwords 3+IHL (bytes 2,3) and 4+IHL (bytes 0,1).
+    // IHL <= 11 keeps them inside the staged 64 bytes; IHL >= 12 needs bytes
+    // 64..77 and takes the rare slow paths below.
+    const uint32_t j = 3u + ihl;
+    const bool tail = j + 1u >= 16u;
+    const uint32_t jj = tail ? 3u : j;
+    const uint32_t pa = mine[(((jj >> 2) ^ rsw) << 2) | (jj & 3u)];
+    const uint32_t pb = mine[((((jj + 1u) >> 2) ^ rsw) << 2) | ((jj + 1u) & 3u)];
 
     // toeplitz_dispatch's checks (ff_dpdk_if.c:1956-1986)
     const uint32_t et = ((d3 & 0xffu) << 8) | ((d3 >> 8) & 0xffu);
+    const bool eth = valid && L >= 14u;
+    const bool ip_ok = eth && et == 0x0800u && L - 14u >= 20u && L - 14u >= ihl4;
     int qv = YRSS_DEFAULT_Q;
-    bool hashed = false;
-    if (valid && L >= 14u) {
-        if (et == 0x0800u) {
-            const uint32_t ip_len = L - 14u;
-            hashed = ip_len >= 20u && ip_len >= ihl4 && (L - ihl4) >= 20u && (d5 >> 24) == 6u;
-        } else if (et == 0x0806u || et == 0x8035u) {
-            qv = 0;
-        }
-    }
+    if (eth && (et == 0x0806u || et == 0x8035u))
+        qv = 0;
+    const bool hashed = ip_ok && (L - ihl4) >= 20u && proto == 6u;
     uint32_t h = 0;
     if (hashed) {
-        // TCP ports at p = 14 + 4*IHL: dwords 3+IHL (bytes 2,3) and 4+IHL (0,1).
-        // IHL <= 11 keeps them inside the staged 64 bytes; IHL >= 12 needs
-        // bytes 64..77 and takes the slow path below.
-        const uint32_t j = 3u + ihl;
-        const bool tail = j + 1u >= 16u;
-        const uint32_t jj = tail ? 3u : j;
-        const uint32_t pa = mine[(((jj >> 2) ^ rsw) << 2) | (jj & 3u)];
-        const uint32_t pb = mine[((((jj + 1u) >> 2) ^ rsw) << 2) | ((jj + 1u) & 3u)];
         // Tuple = LE image of ntohl(src), ntohl(dst), ntohs(sport), ntohs(dport)
         // (ff_dpdk_if.c:1994-2021); 12 byte-table lookups = bit-serial Toeplitz.
         const uint32_t h_l3 =
@@ -214,6 +284,31 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
             h = 0u;
         }
     }
+
+    int fc = kFilterUnknown;
+    if (kFilter) {
+        // protocol_filter (ff_dpdk_if.c:976-996) + ff_kni_proto_filter
+        // (ff_dpdk_kni.c:218-290): ARP, else (KNI on, IPv4) the dst port of the
+        // first TCP/UDP header, recursing through IPIP.
+        bool slow = false;
+        if (eth && et == 0x0806u) {
+            fc = kFilterArp;
+        } else if (P.kni_enable && ip_ok) {
+            const uint32_t nl = L - 14u - ihl4;
+            if (proto == 6u || proto == 17u) {
+                if (nl >= (proto == 6u ? 20u : 8u)) {
+                    if (tail)
+                        slow = true;
+                    else
+                        fc = kni_port_class(kni, proto, pb & 0xffffu);
+                }
+            } else if (proto == 4u) {
+                slow = true;
+            }
+        }
+        if (__builtin_expect(slow, 0))
+            fc = kni_walk(P, kni, mine, rsw, pkt, 14u, L - 14u);
+    }
     // the next tile's ds_writes must not overtake this tile's ds_reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -222,6 +317,8 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
         P.q[pkt] = (int16_t)qv;
         if (P.hash)
             __builtin_nontemporal_store(h, P.hash + pkt);   // never re-read here
+        if (kFilter)
+            P.filter[pkt] = (int8_t)fc;
     }
 
     if (kCount) {
@@ -239,16 +336,15 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 1: parse + Toeplitz hash + queue, one lane per packet.
+// Kernel 1 entry.
 //   kCount   also count packets per bucket per wave segment (compaction on)
-//   kUnroll  tiles whose loads are all issued before the first is processed
-//            (1 or 2; no loaded register is carried across iterations, so
-//            hipcc's vmcnt accounting never has to drain early)
+//   kFilter  also classify protocol_filter / KNI (one byte per packet)
 //   kNT      non-temporal (streaming) window loads
-//   kBlock   workgroup size (256/512/1024): more waves per CU, more bytes in
-//            flight, one 12 KiB table per workgroup
+//   kBlock   workgroup size (256/512): waves per CU, one key table per group
+// LDS: key tables 12 KiB | staging 4 KiB per wave | bucket counters per wave |
+//      KNI bitmaps 16 KiB (kFilter only).
 // ---------------------------------------------------------------------------
-template <bool kCount, int kUnroll, bool kNT, int kBlock>
+template <bool kCount, bool kFilter, bool kNT, int kBlock>
 __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
 {
     constexpr int kWaves = kBlock / kWave;
@@ -257,8 +353,10 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     const uint32_t wave = threadIdx.x / kWave;
     const uint32_t lane = lane_id();
     u32x4 *stage = reinterpret_cast<u32x4 *>(smem + kTblBytes + wave * kStageBytes);
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + kTblBytes + kWaves * kStageBytes) +
-                    wave * P.nb;
+    uint32_t *cnt_base =
+        reinterpret_cast<uint32_t *>(smem + kTblBytes + kWaves * kStageBytes);
+    uint32_t *cnt = cnt_base + wave * P.nb;
+    uint32_t *kni = cnt_base + ((kWaves * P.nb + 3u) & ~3u);
 
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint64_t beg64 = (uint64_t)gw * P.seg;
@@ -267,32 +365,26 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
 
     // Byte tables: tbl[j*256+v] = XOR of key windows at bits 8j+b, v's bit b set.
     for (uint32_t e = threadIdx.x; e < 12u * 256u; e += kBlock) {
-        const uint32_t j = e >> 8, v = e & 255u;
+        const uint32_t jt = e >> 8, v = e & 255u;
         uint32_t acc = 0;
 #pragma unroll
         for (int b = 0; b < 8; ++b)
-            acc ^= (v & (0x80u >> b)) ? P.kwin[8 * j + b] : 0u;
+            acc ^= (v & (0x80u >> b)) ? P.kwin[8 * jt + b] : 0u;
         tbl[e] = acc;
     }
+    if (kFilter)
+        for (uint32_t e = threadIdx.x; e < (uint32_t)kKniWords; e += kBlock)
+            kni[e] = P.kni_enable ? P.kni_bm[e] : 0u;
     if (kCount)
         for (uint32_t b = lane; b < P.nb; b += kWave)
             cnt[b] = 0;
     __syncthreads();
 
-    for (uint32_t t0 = beg; t0 < end; t0 += kUnroll * kTile) {
-        u32x4 r[kUnroll][4];
-        uint32_t L[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint32_t tu = t0 + u * kTile;
-            load_tile<kNT>(P, tu < end ? tu : t0, end, lane, r[u], L[u]);
-        }
-#pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-            const uint32_t tu = t0 + u * kTile;
-            if (u == 0 || tu < end)
-                process_tile<kCount>(P, tbl, stage, cnt, tu, end, lane, r[u], L[u]);
-        }
+    for (uint32_t t0 = beg; t0 < end; t0 += kTile) {
+        u32x4 r[4];
+        uint32_t L;
+        load_tile<kNT>(P, t0, end, lane, r, L);
+        process_tile<kCount, kFilter>(P, tbl, kni, stage, cnt, t0, end, lane, r, L);
     }
 
     if (kCount) {
@@ -504,22 +596,26 @@ struct yrss_ctx {
     yrss_config cfg;
     int device = 0;
     int cus = 0;
-    // parse-kernel launch shape (env overrides for tuning sweeps)
-    // defaults = best of the launch-shape sweep (profiles/r01_sweep_*.json):
-    // non-temporal window loads are worth ~25%; 16 waves/CU of 512-thread
-    // workgroups keep ~64 KiB of loads in flight per CU.
-    uint32_t parse_block = 512;  // YRSS_BLOCK: 256 / 512 / 1024
-    uint32_t unroll = 1;         // YRSS_UNROLL: 1 / 2
+    // Parse-kernel launch shape (env overrides for tuning sweeps).  Defaults =
+    // best of the on-hardware sweep (profiles/r01_sweep_*.json): non-temporal
+    // window loads are worth ~25 %; 16 waves/CU of 512-thread workgroups keep
+    // ~64 KiB of loads in flight per CU.
+    uint32_t parse_block = 512;  // YRSS_BLOCK: 256 / 512
     bool nt = true;              // YRSS_NT
     uint32_t waves_per_cu = 16;  // YRSS_WAVES_PER_CU: cap on resident waves
     uint32_t nb = 0;
-    ParseParams proto{};        // key schedule, modulo constants
-    // compaction workspace, sized for the grid cap
+    ParseParams proto{};         // key schedule, modulo constants
+    // KNI (protocol_filter) state, ff_dpdk_kni.c:60-61 / ff_dpdk_if.c:103-104
+    bool kni_enable = false;
+    bool kni_accept = false;
+    uint8_t kni_bm[2 * 8192] = {};   // tcp bitmap then udp bitmap, htons-indexed
+    uint32_t *d_kni = nullptr;
+    // compaction workspace, sized for the largest grid
     uint32_t seg_cap = 0;
     uint32_t *d_seg_cnt = nullptr;
     uint32_t *d_seg_off = nullptr;
     uint32_t *d_totals = nullptr;
-    // host-burst staging
+    // host-burst staging (pinned) and its device mirror
     hipStream_t stream = nullptr;
     uint32_t burst_cap = 0;
     uint8_t *h_win = nullptr;
@@ -528,12 +624,14 @@ struct yrss_ctx {
     uint32_t *h_hash = nullptr;
     uint32_t *h_qidx = nullptr;
     uint32_t *h_qstart = nullptr;
+    int8_t *h_filter = nullptr;
     uint8_t *d_win = nullptr;
     uint16_t *d_len = nullptr;
     int16_t *d_q = nullptr;
     uint32_t *d_hash = nullptr;
     uint32_t *d_qidx = nullptr;
     uint32_t *d_qstart = nullptr;
+    int8_t *d_filter = nullptr;
     // timing
     uint32_t timing_mask = 0;    // bit k: bracket kernel k with events
     std::vector<hipEvent_t> ev_free;
@@ -557,18 +655,22 @@ int hip_fail(const char *what, hipError_t e)
             return hip_fail(#call, e_);                  \
     } while (0)
 
-size_t parse_lds(const yrss_ctx *c)
+size_t parse_lds(const yrss_ctx *c, bool filter)
 {
     const size_t w = c->parse_block / kWave;
-    return kTblBytes + w * kStageBytes + w * c->nb * sizeof(uint32_t);
+    const size_t cnt = (w * c->nb + 3u) & ~(size_t)3u;
+    return kTblBytes + w * kStageBytes + cnt * sizeof(uint32_t) +
+           (filter ? kKniWords * sizeof(uint32_t) : 0u);
 }
 
+// The grid does not depend on whether the filter is on, so a segment layout
+// (and its compaction) is the same for every variant.
 uint32_t grid_for(const yrss_ctx *c, uint32_t n)
 {
     const uint32_t wpb = c->parse_block / kWave;
     const uint32_t per_block = wpb * kTile;
     const uint32_t want = (n + per_block - 1) / per_block;
-    const uint32_t by_lds = (uint32_t)(160u * 1024u / parse_lds(c));
+    const uint32_t by_lds = (uint32_t)(160u * 1024u / parse_lds(c, true));
     const uint32_t by_waves = std::max(1u, c->waves_per_cu / wpb);
     const uint32_t cap = (uint32_t)c->cus * std::max(1u, std::min(by_lds, by_waves));
     return std::max(1u, std::min(want, cap));
@@ -584,28 +686,24 @@ uint32_t seg_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
 
 typedef void (*ParseKernel)(ParseParams);
 
-template <bool C, int U, bool NT>
+template <bool C, bool F, bool NT>
 ParseKernel pick_block(uint32_t block)
 {
-    switch (block) {
-    case 256: return yrss_parse_hash<C, U, NT, 256>;
-    case 1024: return yrss_parse_hash<C, U, NT, 1024>;
-    default: return yrss_parse_hash<C, U, NT, 512>;
-    }
+    return block == 256 ? yrss_parse_hash<C, F, NT, 256> : yrss_parse_hash<C, F, NT, 512>;
 }
 
-ParseKernel pick_parse(const yrss_ctx *c, bool compact)
+ParseKernel pick_parse(const yrss_ctx *c, bool compact, bool filter)
 {
-    const int v = (compact ? 4 : 0) | (c->unroll == 2 ? 2 : 0) | (c->nt ? 1 : 0);
+    const int v = (compact ? 4 : 0) | (filter ? 2 : 0) | (c->nt ? 1 : 0);
     switch (v) {
-    case 0: return pick_block<false, 1, false>(c->parse_block);
-    case 1: return pick_block<false, 1, true>(c->parse_block);
-    case 2: return pick_block<false, 2, false>(c->parse_block);
-    case 3: return pick_block<false, 2, true>(c->parse_block);
-    case 4: return pick_block<true, 1, false>(c->parse_block);
-    case 5: return pick_block<true, 1, true>(c->parse_block);
-    case 6: return pick_block<true, 2, false>(c->parse_block);
-    default: return pick_block<true, 2, true>(c->parse_block);
+    case 0: return pick_block<false, false, false>(c->parse_block);
+    case 1: return pick_block<false, false, true>(c->parse_block);
+    case 2: return pick_block<false, true, false>(c->parse_block);
+    case 3: return pick_block<false, true, true>(c->parse_block);
+    case 4: return pick_block<true, false, false>(c->parse_block);
+    case 5: return pick_block<true, false, true>(c->parse_block);
+    case 6: return pick_block<true, true, false>(c->parse_block);
+    default: return pick_block<true, true, true>(c->parse_block);
     }
 }
 
@@ -659,16 +757,50 @@ void compute_key_schedule(const yrss_config *cfg, uint32_t kwin[96])
     }
 }
 
+// set_bitmap (ff_dpdk_kni.c:84-89): bit 0x80 >> (p % 8) of byte p / 8, p = htons(port)
+void kni_set_port(uint8_t *bm, uint16_t port)
+{
+    const uint16_t p = (uint16_t)((port << 8) | (port >> 8));
+    bm[p >> 3] |= (uint8_t)(0x80u >> (p & 7u));
+}
+
+// kni_set_bitmap (ff_dpdk_kni.c:99-118), same tokenising rules: a '-' before
+// the next ',' (with at least one character between) makes a range, both ends
+// via atoi; every value goes through the uint16_t of set_bitmap.
+void kni_parse_ports(const char *p, uint8_t *bm)
+{
+    if (!p)
+        return;
+    const char *head = p;
+    for (;;) {
+        const char *tail = strstr(head, ",");
+        const char *tail_num = strstr(head, "-");
+        if (tail_num && (!tail || tail_num < tail - 1)) {
+            const long lo = atoi(head), hi = atoi(tail_num + 1);
+            // a range of 65536+ values sets every bit; bound the loop there
+            for (long i = lo, k = 0; i <= hi && k < 65536; ++i, ++k)
+                kni_set_port(bm, (uint16_t)i);
+        } else {
+            kni_set_port(bm, (uint16_t)atoi(head));
+        }
+        if (!tail)
+            break;
+        head = tail + 1;
+    }
+}
+
 void free_burst(yrss_ctx *c)
 {
     (void)hipHostFree(c->h_win); (void)hipHostFree(c->h_len); (void)hipHostFree(c->h_q);
     (void)hipHostFree(c->h_hash); (void)hipHostFree(c->h_qidx); (void)hipHostFree(c->h_qstart);
+    (void)hipHostFree(c->h_filter);
     (void)hipFree(c->d_win); (void)hipFree(c->d_len); (void)hipFree(c->d_q);
     (void)hipFree(c->d_hash); (void)hipFree(c->d_qidx); (void)hipFree(c->d_qstart);
-    c->h_win = nullptr; c->h_len = nullptr; c->h_q = nullptr;
-    c->h_hash = nullptr; c->h_qidx = nullptr; c->h_qstart = nullptr;
-    c->d_win = nullptr; c->d_len = nullptr; c->d_q = nullptr;
-    c->d_hash = nullptr; c->d_qidx = nullptr; c->d_qstart = nullptr;
+    (void)hipFree(c->d_filter);
+    c->h_win = nullptr; c->h_len = nullptr; c->h_q = nullptr; c->h_hash = nullptr;
+    c->h_qidx = nullptr; c->h_qstart = nullptr; c->h_filter = nullptr;
+    c->d_win = nullptr; c->d_len = nullptr; c->d_q = nullptr; c->d_hash = nullptr;
+    c->d_qidx = nullptr; c->d_qstart = nullptr; c->d_filter = nullptr;
     c->burst_cap = 0;
 }
 
@@ -685,13 +817,94 @@ int ensure_burst(yrss_ctx *c, uint32_t n)
     YRSS_HIP(hipHostMalloc((void **)&c->h_hash, (size_t)cap * 4, hipHostMallocDefault));
     YRSS_HIP(hipHostMalloc((void **)&c->h_qidx, (size_t)cap * 4, hipHostMallocDefault));
     YRSS_HIP(hipHostMalloc((void **)&c->h_qstart, nbk * 4, hipHostMallocDefault));
+    YRSS_HIP(hipHostMalloc((void **)&c->h_filter, (size_t)cap, hipHostMallocDefault));
     YRSS_HIP(hipMalloc((void **)&c->d_win, (size_t)cap * YRSS_WIN_FULL));
     YRSS_HIP(hipMalloc((void **)&c->d_len, (size_t)cap * 2));
     YRSS_HIP(hipMalloc((void **)&c->d_q, (size_t)cap * 2));
     YRSS_HIP(hipMalloc((void **)&c->d_hash, (size_t)cap * 4));
     YRSS_HIP(hipMalloc((void **)&c->d_qidx, (size_t)cap * 4));
     YRSS_HIP(hipMalloc((void **)&c->d_qstart, nbk * 4));
+    YRSS_HIP(hipMalloc((void **)&c->d_filter, (size_t)cap));
     c->burst_cap = cap;
+    return 0;
+}
+
+// Host-staged classification shared by the burst/frames/route entry points.
+// The windows and data_len are already gathered into c->h_win / c->h_len at
+// stride W; results land in the caller's host arrays (NULL = not wanted).
+int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_t *out_hash,
+                    uint32_t *out_qidx, uint32_t *out_qstart, int8_t *out_filter)
+{
+    hipStream_t s = c->stream;
+    const bool compact = out_qidx && out_qstart;
+    YRSS_HIP(hipMemcpyAsync(c->d_win, c->h_win, (size_t)n * W, hipMemcpyHostToDevice, s));
+    YRSS_HIP(hipMemcpyAsync(c->d_len, c->h_len, (size_t)n * 2, hipMemcpyHostToDevice, s));
+    yrss_dev_batch b;
+    b.win = c->d_win;
+    b.win_stride = W;
+    b.n = n;
+    b.len = c->d_len;
+    b.q = c->d_q;
+    b.hash = out_hash ? c->d_hash : nullptr;
+    b.qidx = compact ? c->d_qidx : nullptr;
+    b.qstart = compact ? c->d_qstart : nullptr;
+    b.filter = out_filter ? c->d_filter : nullptr;
+    int rc = yrss_dispatch_dev_ex(c, &b, s);
+    if (rc)
+        return rc;
+    YRSS_HIP(hipMemcpyAsync(c->h_q, c->d_q, (size_t)n * 2, hipMemcpyDeviceToHost, s));
+    if (out_hash)
+        YRSS_HIP(hipMemcpyAsync(c->h_hash, c->d_hash, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    if (out_filter)
+        YRSS_HIP(hipMemcpyAsync(c->h_filter, c->d_filter, n, hipMemcpyDeviceToHost, s));
+    if (compact) {
+        YRSS_HIP(hipMemcpyAsync(c->h_qidx, c->d_qidx, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        YRSS_HIP(hipMemcpyAsync(c->h_qstart, c->d_qstart, (c->nb + 1) * 4,
+                                hipMemcpyDeviceToHost, s));
+    }
+    YRSS_HIP(hipStreamSynchronize(s));
+    memcpy(out_q, c->h_q, (size_t)n * 2);
+    if (out_hash)
+        memcpy(out_hash, c->h_hash, (size_t)n * 4);
+    if (out_filter)
+        memcpy(out_filter, c->h_filter, n);
+    if (compact) {
+        memcpy(out_qidx, c->h_qidx, (size_t)n * 4);
+        memcpy(out_qstart, c->h_qstart, (c->nb + 1) * 4);
+    }
+    return 0;
+}
+
+// Window stride for a host batch: 64 bytes when every frame fits, else 80
+// (enough for any hash; KNI header walks past 80 bytes report TRUNC).
+uint32_t host_stride(uint32_t maxlen) { return maxlen <= YRSS_WIN_MIN ? YRSS_WIN_MIN : YRSS_WIN_FULL; }
+
+// Gather rte_mbuf first-segment headers (rte_pktmbuf_mtod, rte_mbuf.h:1620;
+// rte_pktmbuf_data_len, ff_dpdk_if.c:1076) into the pinned staging.
+int gather_mbufs(yrss_ctx *c, void *const *mbufs, uint32_t n, uint32_t *W_out)
+{
+    int rc = ensure_burst(c, n);
+    if (rc)
+        return rc;
+    const yrss_mbuf_layout &ml = c->cfg.mbuf;
+    uint32_t maxlen = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint16_t L;
+        memcpy(&L, (const uint8_t *)mbufs[i] + ml.off_data_len, 2);
+        c->h_len[i] = L;
+        maxlen = std::max<uint32_t>(maxlen, L);
+    }
+    const uint32_t W = host_stride(maxlen);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *m = (const uint8_t *)mbufs[i];
+        const uint8_t *buf;
+        uint16_t doff;
+        memcpy(&buf, m + ml.off_buf_addr, sizeof(buf));
+        memcpy(&doff, m + ml.off_data_off, 2);
+        const uint32_t L = c->h_len[i];
+        memcpy(c->h_win + (size_t)i * W, buf + doff, L < W ? L : W);
+    }
+    *W_out = W;
     return 0;
 }
 
@@ -777,11 +990,9 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     c->cus = prop.multiProcessorCount;
     if (const char *e = getenv("YRSS_BLOCK")) {
         const int v = atoi(e);
-        if (v == 256 || v == 512 || v == 1024)
+        if (v == 256 || v == 512)
             c->parse_block = (uint32_t)v;
     }
-    if (const char *e = getenv("YRSS_UNROLL"))
-        c->unroll = atoi(e) == 1 ? 1u : 2u;
     if (const char *e = getenv("YRSS_NT"))
         c->nt = atoi(e) != 0;
     if (const char *e = getenv("YRSS_WAVES_PER_CU")) {
@@ -804,6 +1015,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     if ((e = hipMalloc((void **)&c->d_seg_cnt, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_seg_off, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void **)&c->d_kni, sizeof(c->kni_bm))) != hipSuccess ||
+        (e = hipMemset(c->d_kni, 0, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         yrss_fini(c);
         return hip_fail("yrss_init allocation", e);
@@ -833,6 +1046,7 @@ void yrss_fini(yrss_ctx *c)
     (void)hipFree(c->d_seg_cnt);
     (void)hipFree(c->d_seg_off);
     (void)hipFree(c->d_totals);
+    (void)hipFree(c->d_kni);
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
     delete c;
@@ -840,26 +1054,51 @@ void yrss_fini(yrss_ctx *c)
 
 uint32_t yrss_grid_for(yrss_ctx *c, uint32_t n) { return c ? grid_for(c, n) : 0u; }
 
-int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
-                      const uint16_t *d_len, uint32_t n, int16_t *d_q, uint32_t *d_hash,
-                      uint32_t *d_qidx, uint32_t *d_qstart, void *stream)
+int yrss_set_kni(yrss_ctx *c, int enable, const char *method, const char *tcp_ports,
+                 const char *udp_ports)
 {
     if (!c)
         return -EINVAL;
+    bool accept = false;
+    if (method) {
+        // ff_config.c:548-553: method must be accept or reject (case-insensitive)
+        if (strcasecmp(method, "accept") == 0)
+            accept = true;
+        else if (strcasecmp(method, "reject") != 0)
+            return -EINVAL;
+    } else if (enable) {
+        return -EINVAL;                      // ff_config.c:543-546
+    }
+    memset(c->kni_bm, 0, sizeof(c->kni_bm));
+    kni_parse_ports(tcp_ports, c->kni_bm);
+    kni_parse_ports(udp_ports, c->kni_bm + 8192);
+    c->kni_enable = enable != 0;
+    c->kni_accept = accept;
+    YRSS_HIP(hipSetDevice(c->device));
+    YRSS_HIP(hipMemcpy(c->d_kni, c->kni_bm, sizeof(c->kni_bm), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
+{
+    if (!c || !b)
+        return -EINVAL;
+    const uint32_t n = b->n, win_stride = b->win_stride;
     if (win_stride < YRSS_WIN_MIN || (win_stride & 15u))
         return -EINVAL;
-    if (n && (!d_win || !d_len || !d_q))
+    if (n && (!b->win || !b->len || !b->q))
         return -EINVAL;
-    if (((uintptr_t)d_win & 15u) || ((uintptr_t)d_len & 1u) || ((uintptr_t)d_q & 1u) ||
-        ((uintptr_t)d_hash & 3u) || ((uintptr_t)d_qidx & 3u) || ((uintptr_t)d_qstart & 3u))
+    if (((uintptr_t)b->win & 15u) || ((uintptr_t)b->len & 1u) || ((uintptr_t)b->q & 1u) ||
+        ((uintptr_t)b->hash & 3u) || ((uintptr_t)b->qidx & 3u) || ((uintptr_t)b->qstart & 3u))
         return -EINVAL;
-    const bool compact = d_qidx != nullptr;
-    if (compact && !d_qstart)
+    const bool compact = b->qidx != nullptr;
+    const bool filter = b->filter != nullptr;
+    if (compact && !b->qstart)
         return -EINVAL;
     hipStream_t s = (hipStream_t)stream;
     if (n == 0) {
         if (compact)
-            YRSS_HIP(hipMemsetAsync(d_qstart, 0, (c->nb + 1) * sizeof(uint32_t), s));
+            YRSS_HIP(hipMemsetAsync(b->qstart, 0, (c->nb + 1) * sizeof(uint32_t), s));
         return 0;
     }
 
@@ -868,19 +1107,22 @@ int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
     const uint32_t nseg = grid * (c->parse_block / kWave);   // multiple of kScatterWaves
 
     ParseParams P = c->proto;
-    P.win = d_win;
-    P.len = d_len;
-    P.q = d_q;
-    P.hash = d_hash;
+    P.win = b->win;
+    P.len = b->len;
+    P.q = b->q;
+    P.hash = b->hash;
     P.seg_cnt = compact ? c->d_seg_cnt : nullptr;
     P.n = n;
     P.stride = win_stride;
     P.seg = seg;
     P.nseg = nseg;
+    P.filter = b->filter;
+    P.kni_bm = c->d_kni;
+    P.kni_enable = c->kni_enable ? 1u : 0u;
     {
         Timed t(c, s, YRSS_K_PARSE_HASH);
-        hipLaunchKernelGGL(pick_parse(c, compact), dim3(grid), dim3(c->parse_block),
-                           parse_lds(c), s, P);
+        hipLaunchKernelGGL(pick_parse(c, compact, filter), dim3(grid), dim3(c->parse_block),
+                           parse_lds(c, filter), s, P);
     }
     YRSS_HIP(hipGetLastError());
     if (!compact)
@@ -893,11 +1135,11 @@ int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
     }
     YRSS_HIP(hipGetLastError());
     ScatterParams S;
-    S.q = d_q;
+    S.q = b->q;
     S.seg_off = c->d_seg_off;
     S.totals = c->d_totals;
-    S.qidx = d_qidx;
-    S.qstart = d_qstart;
+    S.qidx = b->qidx;
+    S.qstart = b->qstart;
     S.n = n;
     S.seg = seg;
     S.nq = c->cfg.nb_queues;
@@ -912,35 +1154,21 @@ int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
     return 0;
 }
 
-static int burst_common(yrss_ctx *c, uint32_t n, uint32_t wstride, int16_t *out_q,
-                        uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart)
+int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
+                      const uint16_t *d_len, uint32_t n, int16_t *d_q, uint32_t *d_hash,
+                      uint32_t *d_qidx, uint32_t *d_qstart, void *stream)
 {
-    hipStream_t s = c->stream;
-    const bool compact = out_qidx && out_qstart;
-    YRSS_HIP(hipMemcpyAsync(c->d_win, c->h_win, (size_t)n * wstride, hipMemcpyHostToDevice, s));
-    YRSS_HIP(hipMemcpyAsync(c->d_len, c->h_len, (size_t)n * 2, hipMemcpyHostToDevice, s));
-    int rc = yrss_dispatch_dev(c, c->d_win, wstride, c->d_len, n, c->d_q,
-                               out_hash ? c->d_hash : nullptr, compact ? c->d_qidx : nullptr,
-                               compact ? c->d_qstart : nullptr, s);
-    if (rc)
-        return rc;
-    YRSS_HIP(hipMemcpyAsync(c->h_q, c->d_q, (size_t)n * 2, hipMemcpyDeviceToHost, s));
-    if (out_hash)
-        YRSS_HIP(hipMemcpyAsync(c->h_hash, c->d_hash, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-    if (compact) {
-        YRSS_HIP(hipMemcpyAsync(c->h_qidx, c->d_qidx, (size_t)n * 4, hipMemcpyDeviceToHost, s));
-        YRSS_HIP(hipMemcpyAsync(c->h_qstart, c->d_qstart, (c->nb + 1) * 4,
-                                hipMemcpyDeviceToHost, s));
-    }
-    YRSS_HIP(hipStreamSynchronize(s));
-    memcpy(out_q, c->h_q, (size_t)n * 2);
-    if (out_hash)
-        memcpy(out_hash, c->h_hash, (size_t)n * 4);
-    if (compact) {
-        memcpy(out_qidx, c->h_qidx, (size_t)n * 4);
-        memcpy(out_qstart, c->h_qstart, (c->nb + 1) * 4);
-    }
-    return 0;
+    yrss_dev_batch b;
+    b.win = d_win;
+    b.win_stride = win_stride;
+    b.n = n;
+    b.len = d_len;
+    b.q = d_q;
+    b.hash = d_hash;
+    b.qidx = d_qidx;
+    b.qstart = d_qstart;
+    b.filter = nullptr;
+    return yrss_dispatch_dev_ex(c, &b, stream);
 }
 
 int yrss_dispatch_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t *len,
@@ -961,13 +1189,13 @@ int yrss_dispatch_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t
     uint32_t maxlen = 0;
     for (uint32_t i = 0; i < n; ++i)
         maxlen = std::max<uint32_t>(maxlen, len[i]);
-    const uint32_t W = maxlen <= YRSS_WIN_MIN ? YRSS_WIN_MIN : YRSS_WIN_FULL;
+    const uint32_t W = host_stride(maxlen);
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t L = len[i];
         memcpy(c->h_win + (size_t)i * W, data[i], L < W ? L : W);
         c->h_len[i] = (uint16_t)L;
     }
-    return burst_common(c, n, W, out_q, out_hash, out_qidx, out_qstart);
+    return classify_staged(c, n, W, out_q, out_hash, out_qidx, out_qstart, nullptr);
 }
 
 int yrss_dispatch_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out_q,
@@ -982,40 +1210,125 @@ int yrss_dispatch_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *ou
         return 0;
     }
     YRSS_HIP(hipSetDevice(c->device));
-    int rc = ensure_burst(c, n);
+    uint32_t W = 0;
+    int rc = gather_mbufs(c, mbufs, n, &W);
     if (rc)
         return rc;
-    const yrss_mbuf_layout &ml = c->cfg.mbuf;
-    uint32_t maxlen = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t *m = (const uint8_t *)mbufs[i];
-        uint16_t L;
-        memcpy(&L, m + ml.off_data_len, 2);
-        c->h_len[i] = L;
-        maxlen = std::max<uint32_t>(maxlen, L);
-    }
-    const uint32_t W = maxlen <= YRSS_WIN_MIN ? YRSS_WIN_MIN : YRSS_WIN_FULL;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t *m = (const uint8_t *)mbufs[i];
-        const uint8_t *buf;
-        uint16_t doff;
-        memcpy(&buf, m + ml.off_buf_addr, sizeof(buf));
-        memcpy(&doff, m + ml.off_data_off, 2);     // rte_pktmbuf_mtod, rte_mbuf.h:1620
-        const uint32_t L = c->h_len[i];
-        memcpy(c->h_win + (size_t)i * W, buf + doff, L < W ? L : W);
-    }
     uint32_t *hash = out_hash;
     std::vector<uint32_t> tmp;
     if (!hash && (flags & YRSS_F_WRITE_RSS)) {
         tmp.resize(n);
         hash = tmp.data();
     }
-    rc = burst_common(c, n, W, out_q, hash, out_qidx, out_qstart);
+    rc = classify_staged(c, n, W, out_q, hash, out_qidx, out_qstart, nullptr);
     if (rc)
         return rc;
     if (flags & YRSS_F_WRITE_RSS)
         for (uint32_t i = 0; i < n; ++i)
-            memcpy((uint8_t *)mbufs[i] + ml.off_hash_rss, &hash[i], 4);
+            memcpy((uint8_t *)mbufs[i] + c->cfg.mbuf.off_hash_rss, &hash[i], 4);
+    return 0;
+}
+
+int yrss_route_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, uint16_t queue_id,
+                     int kni_primary, const struct yrss_route_ops *ops, void **out_local,
+                     void **out_kni, struct yrss_route_result *res)
+{
+    if (!c || !ops || !ops->enqueue || !ops->clone || !ops->release || !res ||
+        (n && (!mbufs || !out_local || !out_kni)))
+        return -EINVAL;
+    memset(res, 0, sizeof(*res));
+    if (n == 0)
+        return 0;
+    YRSS_HIP(hipSetDevice(c->device));
+    uint32_t W = 0;
+    int rc = gather_mbufs(c, mbufs, n, &W);
+    if (rc)
+        return rc;
+    std::vector<int16_t> q(n);
+    std::vector<int8_t> fc(n);
+    std::vector<uint32_t> qidx(n), qstart(c->nb + 1);
+    rc = classify_staged(c, n, W, q.data(), nullptr, qidx.data(), qstart.data(), fc.data());
+    if (rc)
+        return rc;
+    const uint32_t nq = c->cfg.nb_queues;
+    const bool local_ok = queue_id < nq;
+
+    // ARP packets kept on this lcore are deep-cloned to every other queue
+    // (ff_dpdk_if.c:1099-1119), in packet order, queue order inside a packet,
+    // then once more for KNI when enabled in the primary (:1123-1129).
+    std::vector<uint32_t> arp;               // packet indices, ascending
+    if (local_ok)
+        for (uint32_t k = qstart[queue_id]; k < qstart[queue_id + 1]; ++k)
+            if (fc[qidx[k]] == YRSS_FILTER_ARP)
+                arp.push_back(qidx[k]);
+    std::vector<void *> clones((size_t)arp.size() * nq, nullptr);
+    std::vector<void *> kni_clone(arp.size(), nullptr);
+    for (size_t a = 0; a < arp.size(); ++a) {
+        void *m = mbufs[arp[a]];
+        for (uint16_t j = 0; j < nq; ++j)
+            if (j != queue_id)
+                clones[a * nq + j] = ops->clone(ops->user, m, j);
+        if (c->kni_enable && kni_primary)
+            kni_clone[a] = ops->clone(ops->user, m, 0xFFFFu);
+    }
+
+    // One FIFO burst per ring: that queue's packets merged by packet index with
+    // the ARP clones (a failed clone enqueues nothing, :1114-1118).
+    std::vector<void *> objs;
+    for (uint16_t j = 0; j < nq; ++j) {
+        if (j == queue_id)
+            continue;
+        objs.clear();
+        uint32_t k = qstart[j];
+        const uint32_t e = qstart[j + 1];
+        size_t a = 0;
+        while (k < e || a < arp.size()) {
+            if (a < arp.size() && (k >= e || arp[a] < qidx[k])) {
+                if (clones[a * nq + j])
+                    objs.push_back(clones[a * nq + j]);
+                ++a;
+            } else {
+                objs.push_back(mbufs[qidx[k++]]);
+            }
+        }
+        unsigned done = objs.empty() ? 0u : ops->enqueue(ops->user, j, objs.data(),
+                                                         (unsigned)objs.size());
+        if (done > objs.size())
+            done = (unsigned)objs.size();
+        res->n_ring[j] = done;
+        for (size_t r = done; r < objs.size(); ++r) {      // ring full: free (:1090)
+            ops->release(ops->user, objs[r]);
+            res->n_freed++;
+        }
+    }
+    // ret < 0 || ret >= nb_queues: freed (:1080-1083)
+    for (uint32_t k = qstart[nq]; k < qstart[nq + 1]; ++k) {
+        ops->release(ops->user, mbufs[qidx[k]]);
+        res->n_freed++;
+    }
+    // Local packets, in order: protocol_filter decides (:1096-1138).
+    if (local_ok) {
+        size_t a = 0;
+        for (uint32_t k = qstart[queue_id]; k < qstart[queue_id + 1]; ++k) {
+            const uint32_t i = qidx[k];
+            const int f = fc[i];
+            if (f == YRSS_FILTER_ARP) {
+                if (kni_clone[a])
+                    out_kni[res->n_kni++] = kni_clone[a];
+                ++a;
+                out_local[res->n_local++] = mbufs[i];
+                res->n_arp++;
+            } else if (f == YRSS_FILTER_TRUNC || f == YRSS_FILTER_LOOP) {
+                out_local[res->n_local++] = mbufs[i];
+                res->n_unresolved++;
+            } else if (c->kni_enable && ((f == YRSS_FILTER_KNI && c->kni_accept) ||
+                                         (f == YRSS_FILTER_UNKNOWN && !c->kni_accept))) {
+                out_kni[res->n_kni++] = mbufs[i];
+            } else {
+                out_local[res->n_local++] = mbufs[i];
+            }
+        }
+    }
     return 0;
 }
 

@@ -40,6 +40,7 @@ class DispatchResult:
     hash: object
     qidx: object = None
     qstart: object = None
+    filter: object = None     # protocol_filter class per packet (abi.FILTER_*)
 
     def queue(self, b: int):
         """Indices dispatched to queue b (b == nb_queues: dropped)."""
@@ -121,29 +122,38 @@ class SoftRss:
             stream = torch.cuda.current_stream(self.device)
         return ctypes.c_void_p(stream.cuda_stream)
 
+    # -- KNI / protocol_filter ------------------------------------------------
+    def set_kni(self, enable: bool, method: str | None = "reject", tcp_ports: str | None = None,
+                udp_ports: str | None = None) -> None:
+        """ff_kni_init/init_kni: enable, method accept|reject, port lists."""
+        enc = (lambda x: None if x is None else x.encode())
+        abi.check(self._lib.yrss_set_kni(self._ctx, 1 if enable else 0, enc(method),
+                                         enc(tcp_ports), enc(udp_ports)), "yrss_set_kni")
+
     # -- device-resident path ---------------------------------------------
     def dispatch_dev(self, win, lens, stride: int, n: int | None = None, *,
                      out=None, want_hash: bool = True, compact: bool = True,
-                     stream=None) -> DispatchResult:
-        """Classify n packets resident in HBM (``yrss_dispatch_dev``)."""
-        torch = self._torch()
+                     want_filter: bool = False, stream=None) -> DispatchResult:
+        """Classify n packets resident in HBM (``yrss_dispatch_dev_ex``)."""
         n = int(lens.numel()) if n is None else n
         dev = lens.device
         if out is None:
-            out = self.alloc_out(n, dev, want_hash, compact)
-        rc = self._lib.yrss_dispatch_dev(
-            self._ctx, _ptr(win), stride, _ptr(lens), n, _ptr(out.q),
-            _ptr(out.hash), _ptr(out.qidx), _ptr(out.qstart), self._stream(stream))
-        abi.check(rc, "yrss_dispatch_dev")
+            out = self.alloc_out(n, dev, want_hash, compact, want_filter)
+        b = abi.DevBatch(_ptr(win), stride, n, _ptr(lens), _ptr(out.q), _ptr(out.hash),
+                         _ptr(out.qidx), _ptr(out.qstart), _ptr(out.filter))
+        rc = self._lib.yrss_dispatch_dev_ex(self._ctx, ctypes.byref(b), self._stream(stream))
+        abi.check(rc, "yrss_dispatch_dev_ex")
         return out
 
-    def alloc_out(self, n: int, dev, want_hash=True, compact=True) -> DispatchResult:
+    def alloc_out(self, n: int, dev, want_hash=True, compact=True,
+                  want_filter=False) -> DispatchResult:
         torch = self._torch()
         q = torch.empty(max(n, 1), dtype=torch.int16, device=dev)
         h = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if want_hash else None
         qi = torch.empty(max(n, 1), dtype=torch.int32, device=dev) if compact else None
         qs = torch.empty(self.nb_queues + 2, dtype=torch.int32, device=dev) if compact else None
-        return DispatchResult(q, h, qi, qs)
+        f = torch.empty(max(n, 1), dtype=torch.int8, device=dev) if want_filter else None
+        return DispatchResult(q, h, qi, qs, f)
 
     def synth(self, profile: int, n: int, first: int = 0, seed: int = 0x9E3779B97F4A7C15,
               nflows: int = 1 << 20, stride: int = abi.WIN_MIN, stream=None):
@@ -192,6 +202,35 @@ class SoftRss:
         abi.check(rc, "yrss_dispatch_burst")
         return DispatchResult(q[:n], None if h is None else h[:n],
                               None if qi is None else qi[:n], qs)
+
+    def route_burst(self, mbuf_ptrs: np.ndarray, queue_id: int, enqueue, clone, release,
+                    kni_primary: bool = True):
+        """process_packets' hand-off for a burst (``yrss_route_burst``).
+
+        ``enqueue(queue, [mbuf addr...]) -> n_enqueued``, ``clone(mbuf, queue)
+        -> addr or 0``, ``release(mbuf)`` are called back from C.  Returns
+        (local list, kni list, RouteResult)."""
+        mb = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
+        n = int(mb.size)
+
+        def _enq(user, queue, objs, cnt):
+            return int(enqueue(int(queue), [int(objs[i] or 0) for i in range(cnt)]))
+
+        def _clone(user, m, queue):
+            return int(clone(int(m or 0), int(queue)) or 0)
+
+        def _rel(user, m):
+            release(int(m or 0))
+
+        ops = abi.RouteOps(abi.ENQUEUE_FN(_enq), abi.CLONE_FN(_clone), abi.RELEASE_FN(_rel), None)
+        local = np.zeros(max(n, 1), np.uint64)
+        kni = np.zeros(max(2 * n, 1), np.uint64)
+        res = abi.RouteResult()
+        rc = self._lib.yrss_route_burst(self._ctx, _ptr(mb), n, queue_id, 1 if kni_primary else 0,
+                                        ctypes.byref(ops), _ptr(local), _ptr(kni),
+                                        ctypes.byref(res))
+        abi.check(rc, "yrss_route_burst")
+        return local[:res.n_local].tolist(), kni[:res.n_kni].tolist(), res
 
     # -- timing hook --------------------------------------------------------
     def timing_enable(self, on: bool = True) -> None:
