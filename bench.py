@@ -58,6 +58,8 @@ def parse_args(argv=None):
     ap.add_argument("--dispatch-only-core", type=int, default=1)
     ap.add_argument("--no-compact", action="store_true",
                     help="parse+hash only (no per-queue lists)")
+    ap.add_argument("--filter", action="store_true",
+                    help="also run the fused KNI protocol_filter (1 B/pkt more)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline duration (0 disables)")
     ap.add_argument("--check", type=int, default=1 << 20,
@@ -198,7 +200,10 @@ def main(argv=None):
     first = rank * n                      # weak scaling: rank r owns shard r of the stream
     prof = PROFILES[args.profile]
     win, lens = eng.synth(prof, n, first, SEED, NFLOWS[args.profile], args.stride)
-    out = eng.alloc_out(n, win.device, want_hash=True, compact=not args.no_compact)
+    if args.filter:
+        eng.set_kni(True, "reject", "80,443,8000-8080", "53,123")
+    out = eng.alloc_out(n, win.device, want_hash=True, compact=not args.no_compact,
+                        want_filter=args.filter)
     torch.cuda.synchronize()
 
     def step():
@@ -227,7 +232,7 @@ def main(argv=None):
     # algorithmic bytes per packet for the parse kernel: header window read
     # (min(stride, 64) — the kernel stages 64 B), data_len read (2), hash (4) and
     # queue (2) written = 72 B at 64-B windows.
-    bpp = min(args.stride, 64) + 2 + 4 + 2
+    bpp = min(args.stride, 64) + 2 + 4 + 2 + (1 if args.filter else 0)
     achieved = bpp * n / k_avg_s / 1e9
     key = {"profile": args.profile, "pkts": n, "stride": args.stride,
            "compact": not args.no_compact}
@@ -275,6 +280,7 @@ def main(argv=None):
                 "nb_procs": args.nb_procs, "nb_queues": nbq, "soft_dispatch": 1,
                 "dispatch_only_core": args.dispatch_only_core,
                 "per_queue_lists": not args.no_compact,
+                "kni_filter": args.filter,
                 "parallelism": f"shard{world}",
             },
             "roofline": {

@@ -244,6 +244,52 @@ int yrss_route_burst(yrss_ctx *ctx, void *const *mbufs, uint32_t n, uint16_t que
                      int kni_primary, const struct yrss_route_ops *ops, void **out_local,
                      void **out_kni, struct yrss_route_result *res);
 
+/* ---- connect-side RSS check ----------------------------- */
+
+/* One ff_rss_check call (fs/lib/ff_dpdk_if.c:1904-1940): addresses and ports
+ * exactly as the caller stores them (network byte order, in_pcb.c:1155-1156
+ * passes faddr, laddr, fport, lport). */
+struct yrss_rss_tuple {
+    uint32_t saddr;
+    uint32_t daddr;
+    uint16_t sport;
+    uint16_t dport;
+};
+
+/* For n tuples in HBM: d_ok[i] = ff_rss_check(...) (1 when nb_queues <= 1, else
+ * ((hash & (reta_size - 1)) % nb_queues) == queueid), d_hash[i] (may be NULL)
+ * the Toeplitz hash of the 12 raw tuple bytes.  Asynchronous. */
+int yrss_rss_check_dev(yrss_ctx *ctx, const struct yrss_rss_tuple *d_tuples, uint32_t n,
+                       uint16_t nb_queues, uint16_t reta_size, uint16_t queueid,
+                       uint8_t *d_ok, uint32_t *d_hash, void *stream);
+
+/* The whole ephemeral-port search of in_pcbconnect_setup (in_pcb.c:1131-1170)
+ * in one launch: bit (p & 31) of bitmap[p >> 5] is ff_rss_check(faddr, laddr,
+ * fport, p) for every stored (network-order) lport value p in 0..65535.
+ * bitmap is 2048 host words.  Synchronous. */
+int yrss_rss_lport_sweep(yrss_ctx *ctx, uint32_t faddr, uint32_t laddr, uint16_t fport,
+                         uint16_t nb_queues, uint16_t reta_size, uint16_t queueid,
+                         uint32_t *bitmap);
+
+/* ---- pcap capture I/O ----------------------------------- */
+
+/* ff_enable_pcap + ff_dump_packets (fs/lib/ff_dpdk_pcap.c:49-102) for a burst:
+ * append == 0 creates the file with the reference's 24-byte header (magic
+ * 0xA1B2C3D4, v2.4, snaplen 65535, LINKTYPE_ETHERNET); every frame gets a
+ * 16-byte record {sec, usec, caplen = len, len} and its bytes.  ts_* may be
+ * NULL (zeros).  Host file I/O only. */
+int yrss_pcap_write(const char *path, int append, const uint8_t *const *data,
+                    const uint32_t *len, uint32_t n, const uint32_t *ts_sec,
+                    const uint32_t *ts_usec);
+
+/* Replay: records [first, first+max) of an Ethernet pcap (either byte order,
+ * usec or nsec magic) into header windows of `stride` bytes (>= 64) plus
+ * data_len = min(caplen, 65535) — each record is one single-segment mbuf —
+ * and, if non-NULL, the wire length.  Returns the number of records read, or
+ * -errno.  max == 0 returns the capture's record count. */
+int yrss_pcap_read(const char *path, uint64_t first, uint32_t max, uint8_t *win,
+                   uint32_t stride, uint16_t *len, uint32_t *wire_len);
+
 /* ---- synthetic traffic (bench / parity inputs; see yrss_synth.h) ------------- */
 
 struct yrss_synth_params;

@@ -34,6 +34,15 @@ uint32_t ref_toeplitz_hash(unsigned keylen, const uint8_t *key,
                            unsigned datalen, const uint8_t *data)
 { return toeplitz_hash(keylen, key, datalen, data); }
 const uint8_t *ref_default_rsskey(void) { return default_rsskey_40bytes; }
+/* timing loop for the CPU-baseline calibration (DESIGN.md §6) */
+uint32_t ref_bench_hash(const uint8_t *tuples, unsigned n, unsigned reps)
+{
+    uint32_t acc = 0;
+    for (unsigned r = 0; r < reps; ++r)
+        for (unsigned i = 0; i < n; ++i)
+            acc += toeplitz_hash(40, default_rsskey_40bytes, 12, tuples + 12 * i);
+    return acc;
+}
 EOF
 } | ${CC:-gcc} -O2 -frename-registers -funswitch-loops -fweb -fPIC -shared -x c - \
       -o "$HERE/_ref/libref_thash.so"

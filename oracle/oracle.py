@@ -77,6 +77,9 @@ def lib() -> ctypes.CDLL:
                                              vp, vp]
         L.oracle_filter_windows.restype = None
         L.oracle_filter_windows.argtypes = [vp, u32, vp, u32, ctypes.c_int, vp, vp, vp]
+        L.oracle_rss_check_batch.restype = None
+        L.oracle_rss_check_batch.argtypes = [ctypes.POINTER(OracleCfg), vp, u32, ctypes.c_uint16,
+                                             ctypes.c_uint16, ctypes.c_uint16, vp, vp]
         L.oracle_bench_dispatch.restype = ctypes.c_uint64
         L.oracle_bench_dispatch.argtypes = [vp, u32, vp, u32, ctypes.POINTER(OracleCfg), u32,
                                             ctypes.c_int]
@@ -221,3 +224,32 @@ def process_packets_route(q, fclass, nb_queues, queue_id, kni_enable, kni_accept
         else:
             local.append(("pkt", i))
     return rings, local, kni, freed
+
+
+def rss_check_batch(tuples: np.ndarray, nb_queues: int, reta_size: int, queueid: int,
+                    key: bytes = MLX_KEY):
+    """ff_rss_check over raw 12-byte tuples (uint8 array, n x 12)."""
+    t = np.ascontiguousarray(tuples, dtype=np.uint8).reshape(-1, 12)
+    n = t.shape[0]
+    ok = np.empty(max(n, 1), np.uint8)
+    h = np.empty(max(n, 1), np.uint32)
+    c = cfg(8, 8, 1, 0, key=key)
+    lib().oracle_rss_check_batch(ctypes.byref(c), t.ctypes.data, n, nb_queues, reta_size, queueid,
+                                 ok.ctypes.data, h.ctypes.data)
+    return ok[:n], h[:n]
+
+
+def pcap_bytes(frames, ts_sec=None, ts_usec=None, header: bool = True) -> bytes:
+    """Restatement of ff_enable_pcap + ff_dump_packets (fs/lib/ff_dpdk_pcap.c:49-102):
+    file header {0xA1B2C3D4, 2, 4, 0, 0, 65535, 1}, then per packet
+    {sec, usec, caplen = pkt_len, len = pkt_len} + the segment bytes."""
+    import struct
+
+    out = bytearray()
+    if header:
+        out += struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 0xFFFF, 1)
+    for i, f in enumerate(frames):
+        s = 0 if ts_sec is None else int(ts_sec[i])
+        u = 0 if ts_usec is None else int(ts_usec[i])
+        out += struct.pack("<IIII", s, u, len(f), len(f)) + bytes(f)
+    return bytes(out)

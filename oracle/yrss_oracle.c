@@ -372,3 +372,31 @@ void oracle_filter_windows(const uint8_t *win, uint32_t stride, const uint16_t *
         out[i] = (int8_t)oracle_protocol_filter(win + (size_t)i * stride, len[i], stride,
                                                 enable_kni, tcp_bm, udp_bm);
 }
+
+/* Batch of ff_rss_check calls over raw 12-byte tuples (struct yrss_rss_tuple). */
+void oracle_rss_check_batch(const struct oracle_cfg *c, const uint8_t *tuples, uint32_t n,
+                            uint16_t nb_queues, uint16_t reta_size, uint16_t queueid,
+                            uint8_t *ok, uint32_t *hash)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t s, d;
+        uint16_t sp, dp;
+        memcpy(&s, tuples + 12 * i, 4);
+        memcpy(&d, tuples + 12 * i + 4, 4);
+        memcpy(&sp, tuples + 12 * i + 8, 2);
+        memcpy(&dp, tuples + 12 * i + 10, 2);
+        ok[i] = (uint8_t)oracle_ff_rss_check(c, nb_queues, reta_size, queueid, s, d, sp, dp);
+        if (hash)
+            hash[i] = oracle_toeplitz_hash(c->keylen, c->key, 12, tuples + 12 * i);
+    }
+}
+
+/* timing twin of oracle/_ref's ref_bench_hash (CPU-baseline calibration) */
+uint32_t oracle_bench_hash(const uint8_t *key, const uint8_t *tuples, unsigned n, unsigned reps)
+{
+    uint32_t acc = 0;
+    for (unsigned r = 0; r < reps; ++r)
+        for (unsigned i = 0; i < n; ++i)
+            acc += oracle_toeplitz_hash(40, key, 12, tuples + 12 * i);
+    return acc;
+}

@@ -149,6 +149,13 @@ _PROTOS = {
     "yrss_set_kni": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
                                     ctypes.c_char_p]),
     "yrss_dispatch_dev_ex": (ctypes.c_int, [_vp, ctypes.POINTER(DevBatch), _vp]),
+    "yrss_pcap_write": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, _vp, _vp, _u32, _vp, _vp]),
+    "yrss_pcap_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, _u32, _vp, _u32, _vp,
+                                      _vp]),
+    "yrss_rss_check_dev": (ctypes.c_int, [_vp, _vp, _u32, ctypes.c_uint16, ctypes.c_uint16,
+                                          ctypes.c_uint16, _vp, _vp, _vp]),
+    "yrss_rss_lport_sweep": (ctypes.c_int, [_vp, _u32, _u32, ctypes.c_uint16, ctypes.c_uint16,
+                                            ctypes.c_uint16, ctypes.c_uint16, _vp]),
     "yrss_route_burst": (ctypes.c_int, [_vp, _vp, _u32, ctypes.c_uint16, ctypes.c_int,
                                         ctypes.POINTER(RouteOps), _vp, _vp,
                                         ctypes.POINTER(RouteResult)]),

@@ -547,6 +547,81 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
 }
 
 // ---------------------------------------------------------------------------
+// ff_rss_check (ff_dpdk_if.c:1904-1940) in batch: the connect-side RSS check
+// F-Stack runs per candidate lport in in_pcbconnect_setup (in_pcb.c:1131-1170).
+// The tuple is hashed in its raw stored (network-order) byte order, unlike
+// toeplitz_dispatch's ntohl'd tuple.  One lane per tuple; 12 LDS lookups.
+// ---------------------------------------------------------------------------
+struct RssCheckParams {
+    const yrss_rss_tuple *tuples;   // batch mode
+    uint8_t *ok;
+    uint32_t *hash;
+    uint32_t *bitmap;               // sweep mode: 2048 words
+    uint32_t n;
+    uint32_t fixed[3];              // sweep mode: saddr, daddr, sport (as stored)
+    uint32_t nq;
+    uint32_t mask;                  // (uint32_t)(int)(reta_size - 1)
+    uint32_t queueid;
+    uint32_t sweep;
+    uint32_t kwin[96];
+};
+
+__device__ __forceinline__ uint32_t hash_raw12(const uint32_t *tbl, uint32_t w0, uint32_t w1,
+                                               uint32_t w2)
+{
+    uint32_t h = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        h ^= tbl[(0 + b) * 256 + ((w0 >> (8 * b)) & 0xffu)];
+        h ^= tbl[(4 + b) * 256 + ((w1 >> (8 * b)) & 0xffu)];
+        h ^= tbl[(8 + b) * 256 + ((w2 >> (8 * b)) & 0xffu)];
+    }
+    return h;
+}
+
+__global__ __launch_bounds__(256) void yrss_rss_check(RssCheckParams P)
+{
+    __shared__ uint32_t tbl[12 * 256];
+    for (uint32_t e = threadIdx.x; e < 12u * 256u; e += 256u) {
+        const uint32_t jt = e >> 8, v = e & 255u;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc ^= (v & (0x80u >> b)) ? P.kwin[8 * jt + b] : 0u;
+        tbl[e] = acc;
+    }
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    uint32_t w0, w1, w2;
+    if (P.sweep) {
+        // stored lport value p occupies tuple bytes 10..11 as its little-endian image
+        w0 = P.fixed[0];
+        w1 = P.fixed[1];
+        w2 = (P.fixed[2] & 0xffffu) | ((i & 0xffffu) << 16);
+    } else {
+        const uint32_t k = i < P.n ? i : (P.n ? P.n - 1u : 0u);
+        const uint32_t *t = reinterpret_cast<const uint32_t *>(P.tuples + k);
+        w0 = t[0];
+        w1 = t[1];
+        w2 = t[2];
+    }
+    const uint32_t h = hash_raw12(tbl, w0, w1, w2);
+    const bool ok = P.nq <= 1u || ((h & P.mask) % P.nq) == P.queueid;
+    if (P.sweep) {
+        const uint64_t m = __ballot(ok);
+        const uint32_t lane = lane_id();
+        if (lane == 0)
+            P.bitmap[i >> 5] = (uint32_t)m;
+        else if (lane == 32)
+            P.bitmap[i >> 5] = (uint32_t)(m >> 32);
+    } else if (i < P.n) {
+        P.ok[i] = ok ? 1u : 0u;
+        if (P.hash)
+            P.hash[i] = h;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic traffic straight into HBM (bench / parity input), one thread per
 // packet.  Bit-identical to oracle_synth() on the host.
 // ---------------------------------------------------------------------------
@@ -1329,6 +1404,62 @@ int yrss_route_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, uint16_t queue
             }
         }
     }
+    return 0;
+}
+
+static void rss_check_params(const yrss_ctx *c, uint16_t nb_queues, uint16_t reta_size,
+                             uint16_t queueid, RssCheckParams *P)
+{
+    memset(P, 0, sizeof(*P));
+    memcpy(P->kwin, c->proto.kwin, sizeof(P->kwin));
+    P->nq = nb_queues;
+    P->mask = (uint32_t)((int)reta_size - 1);     // reta_size 0 -> all ones, as in C
+    P->queueid = queueid;
+}
+
+int yrss_rss_check_dev(yrss_ctx *c, const struct yrss_rss_tuple *d_tuples, uint32_t n,
+                       uint16_t nb_queues, uint16_t reta_size, uint16_t queueid, uint8_t *d_ok,
+                       uint32_t *d_hash, void *stream)
+{
+    if (!c || (n && (!d_tuples || !d_ok)) || ((uintptr_t)d_tuples & 3u) ||
+        ((uintptr_t)d_hash & 3u))
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    RssCheckParams P;
+    rss_check_params(c, nb_queues, reta_size, queueid, &P);
+    P.tuples = d_tuples;
+    P.ok = d_ok;
+    P.hash = d_hash;
+    P.n = n;
+    hipLaunchKernelGGL(yrss_rss_check, dim3((n + 255u) / 256u), dim3(256), 0,
+                       (hipStream_t)stream, P);
+    YRSS_HIP(hipGetLastError());
+    return 0;
+}
+
+int yrss_rss_lport_sweep(yrss_ctx *c, uint32_t faddr, uint32_t laddr, uint16_t fport,
+                         uint16_t nb_queues, uint16_t reta_size, uint16_t queueid,
+                         uint32_t *bitmap)
+{
+    if (!c || !bitmap)
+        return -EINVAL;
+    YRSS_HIP(hipSetDevice(c->device));
+    int rc = ensure_burst(c, 2048);
+    if (rc)
+        return rc;
+    RssCheckParams P;
+    rss_check_params(c, nb_queues, reta_size, queueid, &P);
+    P.sweep = 1;
+    P.fixed[0] = faddr;
+    P.fixed[1] = laddr;
+    P.fixed[2] = fport;
+    P.bitmap = c->d_qidx;                     // 8 KiB of the burst staging
+    hipLaunchKernelGGL(yrss_rss_check, dim3(65536 / 256), dim3(256), 0, c->stream, P);
+    YRSS_HIP(hipGetLastError());
+    YRSS_HIP(hipMemcpyAsync(c->h_qidx, c->d_qidx, 2048 * 4, hipMemcpyDeviceToHost, c->stream));
+    YRSS_HIP(hipStreamSynchronize(c->stream));
+    memcpy(bitmap, c->h_qidx, 2048 * 4);
     return 0;
 }
 

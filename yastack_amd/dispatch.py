@@ -232,6 +232,28 @@ class SoftRss:
         abi.check(rc, "yrss_route_burst")
         return local[:res.n_local].tolist(), kni[:res.n_kni].tolist(), res
 
+    # -- connect-side RSS check (ff_rss_check) -------------------------------
+    def rss_check_dev(self, tuples, nb_queues: int, reta_size: int, queueid: int, stream=None):
+        """ff_rss_check for n raw 12-byte tuples on the device (uint8 tensor n*12).
+        Returns (ok uint8 tensor, hash int32 tensor)."""
+        torch = self._torch()
+        n = int(tuples.numel()) // 12
+        ok = torch.empty(max(n, 1), dtype=torch.uint8, device=tuples.device)
+        h = torch.empty(max(n, 1), dtype=torch.int32, device=tuples.device)
+        abi.check(self._lib.yrss_rss_check_dev(self._ctx, _ptr(tuples), n, nb_queues, reta_size,
+                                               queueid, _ptr(ok), _ptr(h), self._stream(stream)),
+                  "yrss_rss_check_dev")
+        return ok[:n], h[:n]
+
+    def rss_lport_sweep(self, faddr: int, laddr: int, fport: int, nb_queues: int,
+                        reta_size: int, queueid: int) -> np.ndarray:
+        """Bitmap (2048 uint32) of every stored lport value accepted by ff_rss_check."""
+        bm = np.zeros(2048, np.uint32)
+        abi.check(self._lib.yrss_rss_lport_sweep(self._ctx, faddr, laddr, fport, nb_queues,
+                                                 reta_size, queueid, _ptr(bm)),
+                  "yrss_rss_lport_sweep")
+        return bm
+
     # -- timing hook --------------------------------------------------------
     def timing_enable(self, on: bool = True) -> None:
         abi.check(self._lib.yrss_timing_enable(self._ctx, 1 if on else 0), "yrss_timing_enable")
