@@ -62,6 +62,9 @@ def parse_args(argv=None):
                     help="also run the fused KNI protocol_filter (1 B/pkt more)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target CPU-baseline duration (0 disables)")
+    ap.add_argument("--pcie", type=int, default=1,
+                    help="also time the host-resident (PCIe-inclusive) paths with "
+                         "tools/yrss_cbench at N=1 (reported beside value, never as value)")
     ap.add_argument("--check", type=int, default=1 << 20,
                     help="packets verified against the oracle after timing (0 = off)")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_parse_hash.json"),
@@ -170,6 +173,32 @@ def probe_traffic(win, lens, out, n, stride, steps):
     return ev[0].elapsed_time(ev[1]) / steps / 1e3
 
 
+def pcie_inclusive(profile: str):
+    """Host-resident rates from tools/yrss_cbench (C host over the C ABI):
+    DPDK-layout mbuf pool of 2^20 packets in host memory, bursts of 32K and 1M."""
+    import subprocess
+
+    exe = ROOT / "tools" / "yrss_cbench"
+    if not exe.exists():
+        return None
+    out = []
+    for burst in (32768, 1 << 20):
+        try:
+            r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
+                               capture_output=True, text=True, timeout=240,
+                               env={**os.environ, "YRSS_CBENCH_MODES": "013"})
+        except subprocess.TimeoutExpired:
+            return None
+        for line in r.stdout.splitlines():
+            try:
+                d = json.loads(line)
+            except ValueError:
+                continue
+            out.append({"api": d["api"], "burst": d["burst"], "mpps": d["mpps"],
+                        "note": d.get("note", "")})
+    return out or None
+
+
 def load_traffic(path: str, key: dict):
     """Per-launch HBM bytes for the parse kernel from a committed PMC summary
     of the same workload (profiles/pmc_parse_hash.json), else None."""
@@ -259,6 +288,10 @@ def main(argv=None):
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, nbq)
+    pcie = None
+    if rank == 0 and world == 1 and args.pcie:
+        eng.close()                       # release the device buffers first
+        pcie = pcie_inclusive(args.profile)
 
     if rank == 0:
         line = {
@@ -296,6 +329,7 @@ def main(argv=None):
                     "parse_frac_of_probe": round(probe_s / k_avg_s, 4)},
             },
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
             "check": check,
         }
         print(json.dumps(line), flush=True)

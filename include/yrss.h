@@ -198,6 +198,35 @@ int yrss_dispatch_burst(yrss_ctx *ctx, void *const *mbufs, uint32_t n,
                         int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx,
                         uint32_t *out_qstart, uint32_t flags);
 
+/* Zero-copy variant: the mbufs (headers and data) live in host memory that was
+ * registered with yrss_register_host_memory (e.g. the DPDK mbuf pool's
+ * memzones).  Only the mbuf pointer array crosses PCIe host->device; a gfx950
+ * kernel reads each mbuf's buf_addr/data_off/data_len and the header window
+ * straight from host memory, and with YRSS_F_WRITE_RSS writes hash.rss back
+ * into the mbuf itself.  The dispatcher core does no per-packet work.
+ * Returns -EFAULT if a mbuf or its data lies outside every registered range
+ * (checked on the GPU; results are then not written). Synchronous. */
+int yrss_dispatch_burst_zc(yrss_ctx *ctx, void *const *mbufs, uint32_t n, int16_t *out_q,
+                           uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                           uint32_t flags);
+
+/* Zero-copy frames: (data pointer, data_len) pairs the host already holds —
+ * e.g. read from the cache-hot mbuf headers right after rte_eth_rx_burst — so
+ * the GPU reads only the header windows from registered host memory (one
+ * 64-byte PCIe read per packet).  Synchronous.
+ *
+ * For both zero-copy calls, pointer/length arrays and output arrays that lie
+ * in registered memory are read and written in place (no staging copies). */
+int yrss_dispatch_frames_zc(yrss_ctx *ctx, const uint8_t *const *data, const uint16_t *len,
+                            uint32_t n, int16_t *out_q, uint32_t *out_hash,
+                            uint32_t *out_qidx, uint32_t *out_qstart);
+
+/* Register / unregister a host range (hipHostRegister, mapped) for the
+ * zero-copy path; up to 16 ranges per context. */
+#define YRSS_MAX_HOST_RANGES 16
+int yrss_register_host_memory(yrss_ctx *ctx, void *base, size_t len);
+int yrss_unregister_host_memory(yrss_ctx *ctx, void *base);
+
 /* Same, for frames given as (data pointer, data_len) pairs. */
 int yrss_dispatch_frames(yrss_ctx *ctx, const uint8_t *const *data,
                          const uint16_t *len, uint32_t n, int16_t *out_q,

@@ -188,9 +188,12 @@ def test_edge_frames_host_api(dev, oracle_mod):
 
 
 def _fake_mbufs(frames, headroom=128):
-    """Lay frames out like an rte_mbuf pool: 128-B mbuf header + headroom + data."""
+    """Lay frames out like an rte_mbuf pool: 128-B mbuf header + headroom + data.
+    The pool is page-aligned (hipHostRegister-able, like a hugepage memzone)."""
     stride = 128 + headroom + 2048 + 64
-    pool = np.zeros(len(frames) * stride, np.uint8)
+    raw = np.zeros(len(frames) * stride + 8192, np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    pool = raw[off: off + len(frames) * stride]
     base = pool.ctypes.data
     ptrs = np.empty(len(frames), np.uint64)
     for i, f in enumerate(frames):
@@ -317,3 +320,75 @@ def test_timing_hook(dev):
         ms2, cnt2 = eng.timing_read(abi.K_SCAN)
         assert cnt2 == 0
         eng.timing_enable(0)
+
+
+@pytest.mark.parametrize("headroom", [128, 131, 134])
+def test_burst_zero_copy(dev, oracle_mod, headroom):
+    """yrss_dispatch_burst_zc: the GPU reads rte_mbuf headers and data from
+    registered host memory (any data alignment), writes hash.rss back."""
+    win, lens = oracle_mod.synth(abi.SYN_FUZZ, 5000, 11, stride=80)
+    frames = []
+    for i in range(5000):
+        L = int(lens[i])
+        f = win[i * 80:(i + 1) * 80].tobytes()
+        frames.append((f + bytes(max(0, L - 80)))[:L] if L <= 2048 else f + bytes(2048 - 80))
+    pool, ptrs, stride = _fake_mbufs(frames, headroom=headroom)
+    c = oracle_mod.cfg(5, 4, 1, 1)
+    want = [oracle_mod.toeplitz_dispatch(f, len(f), c) for f in frames]
+    with SoftRss(5, 4, 1, 1, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        r = eng.dispatch_burst_zc(ptrs, write_rss=True)
+        assert list(r.q) == [q for q, _ in want]
+        assert list(r.hash) == [h for _, h in want]
+        qi_ref, qs_ref = oracle_mod.process_burst(np.array([q for q, _ in want], np.int16), 4)
+        assert np.array_equal(r.qidx, qi_ref) and np.array_equal(r.qstart, qs_ref)
+        rss = pool.reshape(-1, stride)[:, 44:48].copy().view(np.uint32).ravel()
+        assert rss.tolist() == [h for _, h in want]
+        # a pointer outside every registered range is reported, not dereferenced
+        bad = ptrs.copy()
+        bad[17] = np.uint64(pool.ctypes.data + pool.nbytes + 4096)
+        with pytest.raises(abi.YrssError):
+            eng.dispatch_burst_zc(bad)
+        eng.unregister_host_memory(pool.ctypes.data)
+
+
+def test_frames_zero_copy(dev, oracle_mod):
+    """yrss_dispatch_frames_zc with arrays both staged and registered in place."""
+    win, lens = oracle_mod.synth(abi.SYN_FUZZ, 7000, 21, stride=80)
+    frames = []
+    for i in range(7000):
+        L = min(int(lens[i]), 2048)
+        f = win[i * 80:(i + 1) * 80].tobytes()
+        frames.append((f + bytes(max(0, L - 80)))[:L])
+    pool, ptrs, stride = _fake_mbufs(frames, headroom=130)
+    data = (ptrs + np.uint64(128 + 130)).astype(np.uint64)
+    flen = np.array([len(f) for f in frames], np.uint16)
+    c = oracle_mod.cfg(8, 8, 1, 0)
+    want = [oracle_mod.toeplitz_dispatch(f, len(f), c) for f in frames]
+    raw = np.zeros(7000 * 24 + 8192, np.uint8)           # page-aligned arena for in-place arrays
+    off = (-raw.ctypes.data) % 4096
+    arena = raw[off: off + 7000 * 24 + 4096]
+    a_data = arena[:7000 * 8].view(np.uint64)
+    a_len = arena[7000 * 8: 7000 * 10].view(np.uint16)
+    a_q = arena[7000 * 10: 7000 * 12].view(np.int16)
+    a_h = arena[7000 * 12: 7000 * 16].view(np.uint32)
+    a_data[:] = data
+    a_len[:] = flen
+    lib = abi.load()
+    with SoftRss(8, 8, 1, 0, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        # 1) pageable arrays: staged
+        q = np.empty(7000, np.int16)
+        h = np.empty(7000, np.uint32)
+        rc = lib.yrss_dispatch_frames_zc(eng._ctx, data.ctypes.data, flen.ctypes.data, 7000,
+                                         q.ctypes.data, h.ctypes.data, None, None)
+        assert rc == 0
+        assert q.tolist() == [x for x, _ in want] and h.tolist() == [y for _, y in want]
+        # 2) registered arrays: read and written in place by the GPU / DMA
+        eng.register_host_memory(arena.ctypes.data, arena.nbytes)
+        rc = lib.yrss_dispatch_frames_zc(eng._ctx, a_data.ctypes.data, a_len.ctypes.data, 7000,
+                                         a_q.ctypes.data, a_h.ctypes.data, None, None)
+        assert rc == 0
+        assert a_q.tolist() == [x for x, _ in want] and a_h.tolist() == [y for _, y in want]
+        eng.unregister_host_memory(arena.ctypes.data)
+        eng.unregister_host_memory(pool.ctypes.data)

@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <time.h>
 
 #include "yrss.h"
@@ -25,6 +26,21 @@
 #define HEADROOM 128u
 #define DATAROOM 2048u
 #define MBUF_STRIDE (MBUF_HDR + HEADROOM + DATAROOM)   /* 2304: hdr + 2176 buf */
+
+/* data pointer and data_len from each mbuf header (rte_pktmbuf_mtod /
+ * rte_pktmbuf_data_len) — the only per-packet host work of the frames path */
+static void fill_frames(void *const *m, uint32_t n, const uint8_t **data, uint16_t *len)
+{
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *mb = (const uint8_t *)m[i];
+        const uint8_t *buf;
+        uint16_t doff;
+        memcpy(&buf, mb + YRSS_MBUF_OFF_BUF_ADDR, sizeof(buf));
+        memcpy(&doff, mb + YRSS_MBUF_OFF_DATA_OFF, 2);
+        memcpy(&len[i], mb + YRSS_MBUF_OFF_DATA_LEN, 2);
+        data[i] = buf + doff;
+    }
+}
 
 static double now(void)
 {
@@ -40,9 +56,33 @@ int main(int argc, char **argv)
     const uint32_t burst_arg = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
     const double secs = argc > 4 ? atof(argv[4]) : 2.0;
 
-    uint8_t *mem = aligned_alloc(64, (size_t)pool * MBUF_STRIDE);
-    void **mbufs = malloc(sizeof(void *) * pool);
-    if (!mem || !mbufs) {
+    /* DPDK mbuf pools live in hugepage memzones; ask for transparent huge pages
+     * (YRSS_CBENCH_THP=0 keeps 4 KiB pages) so IOMMU translation for the
+     * zero-copy reads sees 2 MiB pages as it would under DPDK */
+    const size_t mem_sz = ((size_t)pool * MBUF_STRIDE + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    const char *thp_env = getenv("YRSS_CBENCH_THP");
+    const int thp = !thp_env || atoi(thp_env) != 0;
+    uint8_t *mem = mmap(NULL, mem_sz + (2u << 20), PROT_READ | PROT_WRITE,
+                        MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (mem == MAP_FAILED)
+        mem = NULL;
+    else {
+        mem = (uint8_t *)(((uintptr_t)mem + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1));
+        if (thp)
+            madvise(mem, mem_sz, MADV_HUGEPAGE);
+    }
+    /* burst-side arrays (mbuf pointers as rte_eth_rx_burst fills them, the frame
+     * pointer/length pairs, and the outputs) in one page-aligned arena that the
+     * zero-copy modes register too, so the GPU reads/writes them in place */
+    const size_t arena_sz = ((size_t)pool * (8 + 8 + 2 + 2 + 4 + 4) + 4096 + 4095) & ~(size_t)4095;
+    uint8_t *arena = aligned_alloc(4096, arena_sz);
+    void **mbufs = (void **)arena;
+    const uint8_t **fdata = (const uint8_t **)(arena + (size_t)pool * 8);
+    uint16_t *flen = (uint16_t *)(arena + (size_t)pool * 16);
+    int16_t *q_all = (int16_t *)(arena + (size_t)pool * 18);
+    uint32_t *h_all = (uint32_t *)(arena + (size_t)pool * 20);
+    uint32_t *qi_all = (uint32_t *)(arena + (size_t)pool * 24);
+    if (!mem || !arena) {
         fprintf(stderr, "out of memory\n");
         return 1;
     }
@@ -69,10 +109,21 @@ int main(int argc, char **argv)
     struct yrss_config cfg;
     yrss_config_default(&cfg);
     const uint32_t bursts[] = {32, 1024, 32768, 1u << 20};
+    static const char *names[4] = {"yrss_dispatch_burst", "yrss_dispatch_burst_zc",
+                                   "yrss_dispatch_frames_zc", "yrss_dispatch_frames_zc"};
+    static const char *notes[4] = {
+        "host gathers 64/80-byte windows into pinned memory, H2D, kernels, D2H",
+        "GPU reads mbuf headers + windows from registered host memory",
+        "host reads data/data_len from each (here cache-cold) mbuf header per burst",
+        "data/data_len arrays already built (as after rte_eth_rx_burst, headers hot)"};
+    const char *mode_env = getenv("YRSS_CBENCH_MODES");    /* e.g. "13" */
+    for (unsigned mode = 0; mode < 4; ++mode)
     for (unsigned bi = 0; bi < sizeof(bursts) / sizeof(bursts[0]); ++bi) {
         const uint32_t B = burst_arg ? burst_arg : bursts[bi];
-        if (B > pool)
+        if (B > pool || (mode_env && !strchr(mode_env, (int)('0' + mode))))
             continue;
+        if (mode == 3)
+            fill_frames(mbufs, pool, fdata, flen);    /* outside the timed region */
         cfg.max_burst = B;
         yrss_ctx *ctx = NULL;
         int rc = yrss_init(&cfg, &ctx);
@@ -80,13 +131,23 @@ int main(int argc, char **argv)
             fprintf(stderr, "yrss_init: %d\n", rc);
             return 2;
         }
-        int16_t *q = malloc(sizeof(int16_t) * B);
-        uint32_t *h = malloc(sizeof(uint32_t) * B);
-        uint32_t *qi = malloc(sizeof(uint32_t) * B);
+        if (mode >= 1 && ((rc = yrss_register_host_memory(ctx, mem, mem_sz)) ||
+                          (rc = yrss_register_host_memory(ctx, arena, arena_sz)))) {
+            fprintf(stderr, "yrss_register_host_memory: %d\n", rc);
+            return 2;
+        }
+        int16_t *q = q_all;
+        uint32_t *h = h_all, *qi = qi_all;
         uint32_t qs[YRSS_MAX_QUEUES + 2];
+        /* one burst: what the dispatcher lcore would do after rte_eth_rx_burst */
+        #define RUN_BURST(off) ( \
+            mode == 0 ? yrss_dispatch_burst(ctx, mbufs + (off), B, q, h, qi, qs, 0) : \
+            mode == 1 ? yrss_dispatch_burst_zc(ctx, mbufs + (off), B, q, h, qi, qs, 0) : \
+            ((mode == 2 ? fill_frames(mbufs + (off), B, fdata + (off), flen + (off)) : (void)0), \
+             yrss_dispatch_frames_zc(ctx, fdata + (off), flen + (off), B, q, h, qi, qs)))
         /* warm up */
         for (uint32_t off = 0; off + B <= pool && off < 4 * B; off += B)
-            if ((rc = yrss_dispatch_burst(ctx, mbufs + off, B, q, h, qi, qs, 0)) != 0) {
+            if ((rc = RUN_BURST(off)) != 0) {
                 fprintf(stderr, "dispatch: %d\n", rc);
                 return 3;
             }
@@ -97,7 +158,7 @@ int main(int argc, char **argv)
         while (t1 - t0 < secs) {
             if (off + B > pool)
                 off = 0;
-            rc = yrss_dispatch_burst(ctx, mbufs + off, B, q, h, qi, qs, 0);
+            rc = RUN_BURST(off);
             if (rc) {
                 fprintf(stderr, "dispatch: %d\n", rc);
                 return 3;
@@ -106,20 +167,18 @@ int main(int argc, char **argv)
             pkts += B;
             t1 = now();
         }
-        printf("{\"tool\": \"yrss_cbench\", \"api\": \"yrss_dispatch_burst\", \"profile\": %u, "
+        printf("{\"tool\": \"yrss_cbench\", \"api\": \"%s\", \"profile\": %u, "
                "\"burst\": %u, \"pkts\": %llu, \"seconds\": %.3f, \"mpps\": %.2f, "
-               "\"us_per_burst\": %.2f, \"queue_of_first\": %d}\n",
-               profile, B, (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
-               (t1 - t0) / (pkts / (double)B) * 1e6, q[0]);
+               "\"us_per_burst\": %.2f, \"queue_of_first\": %d, \"thp\": %d, "
+               "\"mode\": %u, \"note\": \"%s\"}\n",
+               names[mode], profile, B,
+               (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
+               (t1 - t0) / (pkts / (double)B) * 1e6, q[0], thp, mode, notes[mode]);
         fflush(stdout);
-        free(q);
-        free(h);
-        free(qi);
-        yrss_fini(ctx);
+        yrss_fini(ctx);                 /* also unregisters the pool */
         if (burst_arg)
             break;
     }
-    free(mbufs);
-    free(mem);
+    free(arena);
     return 0;
 }

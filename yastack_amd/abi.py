@@ -149,6 +149,10 @@ _PROTOS = {
     "yrss_set_kni": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
                                     ctypes.c_char_p]),
     "yrss_dispatch_dev_ex": (ctypes.c_int, [_vp, ctypes.POINTER(DevBatch), _vp]),
+    "yrss_dispatch_burst_zc": (ctypes.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32]),
+    "yrss_dispatch_frames_zc": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp]),
+    "yrss_register_host_memory": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    "yrss_unregister_host_memory": (ctypes.c_int, [_vp, _vp]),
     "yrss_pcap_write": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, _vp, _vp, _u32, _vp, _vp]),
     "yrss_pcap_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, _u32, _vp, _u32, _vp,
                                       _vp]),

@@ -622,6 +622,140 @@ __global__ __launch_bounds__(256) void yrss_rss_check(RssCheckParams P)
 }
 
 // ---------------------------------------------------------------------------
+// Zero-copy gather: header windows straight out of host-resident rte_mbufs.
+// Four lanes per packet: one wave-instruction reads the first 64 bytes of 16
+// mbuf headers (one 64-byte PCIe read each), the quad exchanges buf_addr /
+// data_off / data_len by shuffles, then reads the packet's header window the
+// same way (rte_pktmbuf_mtod, rte_mbuf.h:1620) and stores it to HBM in the
+// yrss_dispatch_dev layout (stride 80).
+// ---------------------------------------------------------------------------
+struct HostRange {
+    uint64_t lo, hi;      // host virtual range [lo, hi)
+    int64_t delta;        // device address = host address + delta
+};
+
+struct GatherParams {
+    const uint64_t *ptrs;       // mbuf (or frame data) pointers, device-visible
+    const uint16_t *lens;       // frames mode: data_len per frame, device-visible
+    uint8_t *win;               // n x 80
+    uint16_t *len;
+    uint32_t *fault;            // set when a pointer is outside every range
+    const uint32_t *hash;       // write-back mode: hash per packet
+    uint32_t n;
+    uint32_t nranges;
+    uint32_t off_buf_addr, off_data_off, off_data_len, off_hash_rss;
+    uint32_t frames;            // 1: ptrs are frame data pointers, lens given
+    HostRange ranges[YRSS_MAX_HOST_RANGES];
+};
+
+__device__ __forceinline__ bool host_xlate(const GatherParams &G, uint64_t a, uint32_t bytes,
+                                           int64_t *delta)
+{
+    for (uint32_t r = 0; r < G.nranges; ++r)
+        if (a >= G.ranges[r].lo && a + bytes <= G.ranges[r].hi) {
+            *delta = G.ranges[r].delta;
+            return true;
+        }
+    return false;
+}
+
+// 16 bytes from host memory at any alignment (DPDK data is normally 64-byte
+// aligned; rte_pktmbuf_adj can leave it anywhere).
+__device__ __forceinline__ u32x4 host_load16(uint64_t a)
+{
+    if ((a & 15u) == 0)
+        return *reinterpret_cast<const u32x4 *>(a);
+    u32x4 v;
+    if ((a & 3u) == 0) {
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(a);
+        v.x = p[0]; v.y = p[1]; v.z = p[2]; v.w = p[3];
+        return v;
+    }
+    const uint8_t *b = reinterpret_cast<const uint8_t *>(a);
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        w[k] = b[4 * k] | (b[4 * k + 1] << 8) | (b[4 * k + 2] << 16) | ((uint32_t)b[4 * k + 3] << 24);
+    v.x = w[0]; v.y = w[1]; v.z = w[2]; v.w = w[3];
+    return v;
+}
+
+__device__ __forceinline__ uint32_t pick_word(const u32x4 &v, uint32_t k)
+{
+    return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+}
+
+// dword at byte offset o (4-aligned, < 64) of the quad's 64-byte header
+__device__ __forceinline__ uint32_t quad_word(const u32x4 &hv, uint32_t lane, uint32_t o)
+{
+    return __shfl(pick_word(hv, (o >> 2) & 3u), (int)((lane & ~3u) | (o >> 4)), kWave);
+}
+
+__global__ __launch_bounds__(256) void yrss_gather_zc(GatherParams G)
+{
+    const uint32_t lane = lane_id(), c = lane & 3u;
+    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) / kWave;
+    const uint32_t nwaves = gridDim.x * (256u / kWave);
+    for (uint32_t p0 = wave * 16u; p0 < G.n; p0 += nwaves * 16u) {
+        const uint32_t i = p0 + (lane >> 2);
+        const bool valid = i < G.n;
+        const uint64_t m = valid ? G.ptrs[i] : 0u;
+        uint64_t data;
+        uint32_t L;
+        bool ok_m;
+        if (G.frames) {
+            // frames mode: the host already knows data pointer and data_len
+            data = m;
+            L = valid ? G.lens[i] : 0u;
+            ok_m = valid;
+        } else {
+            int64_t dm = 0;
+            ok_m = valid && host_xlate(G, m, 64u, &dm);
+            u32x4 hv = {0u, 0u, 0u, 0u};
+            if (ok_m)
+                hv = host_load16(m + dm + 16u * c);
+            const uint32_t ob = G.off_buf_addr, od = G.off_data_off, ol = G.off_data_len;
+            const uint64_t buf = (uint64_t)quad_word(hv, lane, ob) |
+                                 ((uint64_t)quad_word(hv, lane, ob + 4u) << 32);
+            const uint32_t doff = (quad_word(hv, lane, od & ~3u) >> (8u * (od & 3u))) & 0xffffu;
+            L = (quad_word(hv, lane, ol & ~3u) >> (8u * (ol & 3u))) & 0xffffu;
+            data = buf + doff;
+        }
+        const uint32_t need = (min(L, (uint32_t)YRSS_WIN_FULL) + 15u) & ~15u;   // bytes to read
+        int64_t dd = 0;
+        const bool ok_d = ok_m && (need == 0 || host_xlate(G, data, need, &dd));
+        uint8_t *dst = G.win + (size_t)i * YRSS_WIN_FULL;
+        if (valid) {
+            u32x4 w = {0u, 0u, 0u, 0u};
+            if (ok_d && 16u * c < need)
+                w = host_load16(data + dd + 16u * c);
+            *reinterpret_cast<u32x4 *>(dst + 16u * c) = w;
+            if (c == 0) {
+                u32x4 t = {0u, 0u, 0u, 0u};
+                if (ok_d && need > 64u)
+                    t = host_load16(data + dd + 64u);
+                *reinterpret_cast<u32x4 *>(dst + 64u) = t;
+                G.len[i] = (uint16_t)L;
+                if (!ok_d)
+                    atomicOr(G.fault, 1u);
+            }
+        }
+    }
+}
+
+// hash.rss write-back straight into the host mbufs (YRSS_F_WRITE_RSS)
+__global__ __launch_bounds__(256) void yrss_writeback_zc(GatherParams G)
+{
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= G.n)
+        return;
+    const uint64_t m = G.ptrs[i];
+    int64_t dm = 0;
+    if (host_xlate(G, m, G.off_hash_rss + 4u, &dm))
+        *reinterpret_cast<uint32_t *>(m + dm + G.off_hash_rss) = G.hash[i];
+}
+
+// ---------------------------------------------------------------------------
 // Synthetic traffic straight into HBM (bench / parity input), one thread per
 // packet.  Bit-identical to oracle_synth() on the host.
 // ---------------------------------------------------------------------------
@@ -707,6 +841,14 @@ struct yrss_ctx {
     uint32_t *d_qidx = nullptr;
     uint32_t *d_qstart = nullptr;
     int8_t *d_filter = nullptr;
+    // zero-copy: registered host ranges, device pointer array and fault word
+    uint32_t nranges = 0;
+    HostRange ranges[YRSS_MAX_HOST_RANGES] = {};
+    void *range_base[YRSS_MAX_HOST_RANGES] = {};
+    uint64_t *h_ptrs = nullptr;
+    uint64_t *d_ptrs = nullptr;
+    uint32_t *d_fault = nullptr;
+    uint32_t *h_fault = nullptr;
     // timing
     uint32_t timing_mask = 0;    // bit k: bracket kernel k with events
     std::vector<hipEvent_t> ev_free;
@@ -869,6 +1011,10 @@ void free_burst(yrss_ctx *c)
     (void)hipHostFree(c->h_win); (void)hipHostFree(c->h_len); (void)hipHostFree(c->h_q);
     (void)hipHostFree(c->h_hash); (void)hipHostFree(c->h_qidx); (void)hipHostFree(c->h_qstart);
     (void)hipHostFree(c->h_filter);
+    (void)hipHostFree(c->h_ptrs);
+    (void)hipFree(c->d_ptrs);
+    c->h_ptrs = nullptr;
+    c->d_ptrs = nullptr;
     (void)hipFree(c->d_win); (void)hipFree(c->d_len); (void)hipFree(c->d_q);
     (void)hipFree(c->d_hash); (void)hipFree(c->d_qidx); (void)hipFree(c->d_qstart);
     (void)hipFree(c->d_filter);
@@ -900,6 +1046,8 @@ int ensure_burst(yrss_ctx *c, uint32_t n)
     YRSS_HIP(hipMalloc((void **)&c->d_qidx, (size_t)cap * 4));
     YRSS_HIP(hipMalloc((void **)&c->d_qstart, nbk * 4));
     YRSS_HIP(hipMalloc((void **)&c->d_filter, (size_t)cap));
+    YRSS_HIP(hipHostMalloc((void **)&c->h_ptrs, (size_t)cap * 8, hipHostMallocDefault));
+    YRSS_HIP(hipMalloc((void **)&c->d_ptrs, (size_t)cap * 8));
     c->burst_cap = cap;
     return 0;
 }
@@ -1091,6 +1239,9 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         (e = hipMalloc((void **)&c->d_seg_off, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_kni, sizeof(c->kni_bm))) != hipSuccess ||
+        (e = hipMalloc((void **)&c->d_fault, sizeof(uint32_t))) != hipSuccess ||
+        (e = hipHostMalloc((void **)&c->h_fault, sizeof(uint32_t), hipHostMallocDefault)) !=
+            hipSuccess ||
         (e = hipMemset(c->d_kni, 0, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         yrss_fini(c);
@@ -1122,6 +1273,10 @@ void yrss_fini(yrss_ctx *c)
     (void)hipFree(c->d_seg_off);
     (void)hipFree(c->d_totals);
     (void)hipFree(c->d_kni);
+    (void)hipFree(c->d_fault);
+    (void)hipHostFree(c->h_fault);
+    for (uint32_t r = 0; r < c->nranges; ++r)
+        (void)hipHostUnregister(c->range_base[r]);
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1302,6 +1457,179 @@ int yrss_dispatch_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *ou
         for (uint32_t i = 0; i < n; ++i)
             memcpy((uint8_t *)mbufs[i] + c->cfg.mbuf.off_hash_rss, &hash[i], 4);
     return 0;
+}
+
+int yrss_register_host_memory(yrss_ctx *c, void *base, size_t len)
+{
+    if (!c || !base || !len || c->nranges >= YRSS_MAX_HOST_RANGES)
+        return -EINVAL;
+    YRSS_HIP(hipSetDevice(c->device));
+    YRSS_HIP(hipHostRegister(base, len, hipHostRegisterMapped));
+    void *dev = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&dev, base, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(base);
+        return hip_fail("hipHostGetDevicePointer", e);
+    }
+    HostRange &r = c->ranges[c->nranges];
+    r.lo = (uint64_t)(uintptr_t)base;
+    r.hi = r.lo + len;
+    r.delta = (int64_t)((uintptr_t)dev - (uintptr_t)base);
+    c->range_base[c->nranges++] = base;
+    return 0;
+}
+
+int yrss_unregister_host_memory(yrss_ctx *c, void *base)
+{
+    if (!c)
+        return -EINVAL;
+    for (uint32_t r = 0; r < c->nranges; ++r)
+        if (c->range_base[r] == base) {
+            YRSS_HIP(hipSetDevice(c->device));
+            YRSS_HIP(hipHostUnregister(base));
+            for (uint32_t k = r + 1; k < c->nranges; ++k) {
+                c->ranges[k - 1] = c->ranges[k];
+                c->range_base[k - 1] = c->range_base[k];
+            }
+            --c->nranges;
+            return 0;
+        }
+    return -EINVAL;
+}
+
+namespace {
+
+// Device-visible alias of host bytes [p, p+bytes) if they lie in a registered
+// range, else nullptr.
+const void *dev_alias(const yrss_ctx *c, const void *p, size_t bytes)
+{
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    for (uint32_t r = 0; r < c->nranges; ++r)
+        if (a >= c->ranges[r].lo && a + bytes <= c->ranges[r].hi)
+            return (const void *)(uintptr_t)(a + c->ranges[r].delta);
+    return nullptr;
+}
+
+// D2H into a caller array: straight DMA when the array is registered (pinned),
+// else through the pinned staging (then copied after the sync).
+struct Out {
+    void *user;
+    void *stage;
+    size_t bytes;
+    bool direct;
+};
+
+int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n, bool frames,
+                int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                uint32_t flags)
+{
+    const yrss_mbuf_layout &ml = c->cfg.mbuf;
+    if (!frames && (ml.off_buf_addr % 8u || ml.off_buf_addr + 8u > 64u || ml.off_data_off % 2u ||
+                    ml.off_data_off + 2u > 64u || ml.off_data_len % 2u ||
+                    ml.off_data_len + 2u > 64u || ml.off_hash_rss % 4u))
+        return -EINVAL;                      // header fields must sit in the first 64 bytes
+    if (n == 0) {
+        if (out_qstart)
+            memset(out_qstart, 0, (c->nb + 1) * sizeof(uint32_t));
+        return 0;
+    }
+    YRSS_HIP(hipSetDevice(c->device));
+    int rc = ensure_burst(c, n);
+    if (rc)
+        return rc;
+    hipStream_t s = c->stream;
+    GatherParams G;
+    memset(&G, 0, sizeof(G));
+    // the pointer (and length) arrays are read in place when registered
+    G.ptrs = (const uint64_t *)dev_alias(c, ptrs, (size_t)n * 8);
+    if (!G.ptrs) {
+        memcpy(c->h_ptrs, ptrs, (size_t)n * 8);
+        YRSS_HIP(hipMemcpyAsync(c->d_ptrs, c->h_ptrs, (size_t)n * 8, hipMemcpyHostToDevice, s));
+        G.ptrs = c->d_ptrs;
+    }
+    if (frames) {
+        G.lens = (const uint16_t *)dev_alias(c, lens, (size_t)n * 2);
+        if (!G.lens) {
+            memcpy(c->h_len, lens, (size_t)n * 2);
+            YRSS_HIP(hipMemcpyAsync(c->d_q, c->h_len, (size_t)n * 2, hipMemcpyHostToDevice, s));
+            G.lens = (const uint16_t *)c->d_q;   // d_q is free until the parse kernel
+        }
+    }
+    YRSS_HIP(hipMemsetAsync(c->d_fault, 0, sizeof(uint32_t), s));
+    G.win = c->d_win;
+    G.len = c->d_len;
+    G.fault = c->d_fault;
+    G.hash = c->d_hash;
+    G.n = n;
+    G.frames = frames ? 1u : 0u;
+    G.nranges = c->nranges;
+    G.off_buf_addr = ml.off_buf_addr;
+    G.off_data_off = ml.off_data_off;
+    G.off_data_len = ml.off_data_len;
+    G.off_hash_rss = ml.off_hash_rss;
+    memcpy(G.ranges, c->ranges, sizeof(G.ranges));
+    const uint32_t blocks = std::min<uint32_t>((n + 63u) / 64u, (uint32_t)c->cus * 8u);
+    hipLaunchKernelGGL(yrss_gather_zc, dim3(blocks), dim3(256), 0, s, G);
+    YRSS_HIP(hipGetLastError());
+    const bool compact = out_qidx && out_qstart;
+    const bool want_hash = out_hash || (flags & YRSS_F_WRITE_RSS);
+    yrss_dev_batch b;
+    b.win = c->d_win;
+    b.win_stride = YRSS_WIN_FULL;
+    b.n = n;
+    b.len = c->d_len;
+    b.q = c->d_q;
+    b.hash = want_hash ? c->d_hash : nullptr;
+    b.qidx = compact ? c->d_qidx : nullptr;
+    b.qstart = compact ? c->d_qstart : nullptr;
+    b.filter = nullptr;
+    if ((rc = yrss_dispatch_dev_ex(c, &b, s)) != 0)
+        return rc;
+    if (!frames && (flags & YRSS_F_WRITE_RSS)) {
+        hipLaunchKernelGGL(yrss_writeback_zc, dim3((n + 255u) / 256u), dim3(256), 0, s, G);
+        YRSS_HIP(hipGetLastError());
+    }
+    Out outs[4] = {{out_q, c->h_q, (size_t)n * 2, false},
+                   {out_hash, c->h_hash, (size_t)n * 4, false},
+                   {compact ? out_qidx : nullptr, c->h_qidx, (size_t)n * 4, false},
+                   {compact ? out_qstart : nullptr, c->h_qstart, (c->nb + 1) * 4, false}};
+    const void *src[4] = {c->d_q, c->d_hash, c->d_qidx, c->d_qstart};
+    YRSS_HIP(hipMemcpyAsync(c->h_fault, c->d_fault, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    for (int k = 0; k < 4; ++k) {
+        if (!outs[k].user)
+            continue;
+        outs[k].direct = dev_alias(c, outs[k].user, outs[k].bytes) != nullptr;
+        YRSS_HIP(hipMemcpyAsync(outs[k].direct ? outs[k].user : outs[k].stage, src[k],
+                                outs[k].bytes, hipMemcpyDeviceToHost, s));
+    }
+    YRSS_HIP(hipStreamSynchronize(s));
+    if (*c->h_fault)
+        return -EFAULT;
+    for (int k = 0; k < 4; ++k)
+        if (outs[k].user && !outs[k].direct)
+            memcpy(outs[k].user, outs[k].stage, outs[k].bytes);
+    return 0;
+}
+
+}  // namespace
+
+int yrss_dispatch_burst_zc(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out_q,
+                           uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                           uint32_t flags)
+{
+    if (!c || (n && (!mbufs || !out_q)))
+        return -EINVAL;
+    return zc_dispatch(c, mbufs, nullptr, n, false, out_q, out_hash, out_qidx, out_qstart,
+                       flags);
+}
+
+int yrss_dispatch_frames_zc(yrss_ctx *c, const uint8_t *const *data, const uint16_t *len,
+                            uint32_t n, int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx,
+                            uint32_t *out_qstart)
+{
+    if (!c || (n && (!data || !len || !out_q)))
+        return -EINVAL;
+    return zc_dispatch(c, data, len, n, true, out_q, out_hash, out_qidx, out_qstart, 0);
 }
 
 int yrss_route_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, uint16_t queue_id,

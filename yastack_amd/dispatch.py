@@ -203,6 +203,29 @@ class SoftRss:
         return DispatchResult(q[:n], None if h is None else h[:n],
                               None if qi is None else qi[:n], qs)
 
+    def register_host_memory(self, base: int, nbytes: int) -> None:
+        abi.check(self._lib.yrss_register_host_memory(self._ctx, base, nbytes),
+                  "yrss_register_host_memory")
+
+    def unregister_host_memory(self, base: int) -> None:
+        abi.check(self._lib.yrss_unregister_host_memory(self._ctx, base),
+                  "yrss_unregister_host_memory")
+
+    def dispatch_burst_zc(self, mbuf_ptrs: np.ndarray, want_hash=True, compact=True,
+                          write_rss=False) -> DispatchResult:
+        """Zero-copy burst: mbufs in registered host memory are read by the GPU."""
+        mb = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
+        n = int(mb.size)
+        q = np.empty(max(n, 1), np.int16)
+        h = np.empty(max(n, 1), np.uint32) if want_hash else None
+        qi = np.empty(max(n, 1), np.uint32) if compact else None
+        qs = np.empty(self.nb_queues + 2, np.uint32) if compact else None
+        rc = self._lib.yrss_dispatch_burst_zc(self._ctx, _ptr(mb), n, _ptr(q), _ptr(h), _ptr(qi),
+                                              _ptr(qs), abi.F_WRITE_RSS if write_rss else 0)
+        abi.check(rc, "yrss_dispatch_burst_zc")
+        return DispatchResult(q[:n], None if h is None else h[:n],
+                              None if qi is None else qi[:n], qs)
+
     def route_burst(self, mbuf_ptrs: np.ndarray, queue_id: int, enqueue, clone, release,
                     kni_primary: bool = True):
         """process_packets' hand-off for a burst (``yrss_route_burst``).
