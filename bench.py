@@ -77,6 +77,8 @@ def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if os.environ.get("YRSS_BENCH_ONE_DEVICE"):
+        local = 0            # rehearsal of the N>1 path on a single GPU
     if world > 1:
         import torch.distributed as dist
 
