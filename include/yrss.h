@@ -62,9 +62,11 @@ extern "C" {
 /* Minimum window stride: one 64-byte coalesced header block per packet. */
 #define YRSS_WIN_MIN 64
 
-/* Largest supported values (queues are buckets of the compaction; q is int16). */
+/* Largest supported values (queues are buckets of the compaction; q is int16;
+ * packet indices stay well inside uint32 arithmetic). */
 #define YRSS_MAX_QUEUES 256
 #define YRSS_MAX_PROCS 4096
+#define YRSS_MAX_BATCH (1u << 31)
 
 /* struct rte_mbuf field offsets for the in-tree DPDK 18.02 (x86_64), measured
  * from dpdk/lib/librte_mbuf/rte_mbuf.h:412-560.  The burst API reads
@@ -142,7 +144,7 @@ void yrss_fini(yrss_ctx *ctx);
  *              ff_dpdk_if.c:1080-1083).  Bucket b = d_qidx[d_qstart[b] ..
  *              d_qstart[b+1]).  d_qstart[nb_queues+1] == n.
  *   stream     hipStream_t (NULL = legacy default stream)
- * Asynchronous: returns after enqueueing the kernels. */
+ * n <= YRSS_MAX_BATCH.  Asynchronous: returns after enqueueing the kernels. */
 int yrss_dispatch_dev(yrss_ctx *ctx, const uint8_t *d_win, uint32_t win_stride,
                       const uint16_t *d_len, uint32_t n, int16_t *d_q,
                       uint32_t *d_hash, uint32_t *d_qidx, uint32_t *d_qstart,

@@ -48,6 +48,7 @@ constexpr int kScatterBlock = 256;     // 4 waves (segments) per workgroup
 constexpr int kScatterWaves = kScatterBlock / kWave;
 constexpr int kMaxWavesPerCU = 32;
 constexpr int kScatterRound = 8;       // packets per lane per scatter round
+constexpr uint32_t kFewBuckets = 6;    // scatter: distinct-bucket loop up to this many
 constexpr int kTblBytes = 12 * 256 * 4;
 constexpr int kStageBytes = kTile * 64; // 4 KiB per wave
 
@@ -77,6 +78,7 @@ struct ParseParams {
 struct ScatterParams {
     const int16_t *q;
     const uint32_t *seg_off;   // [nb][nseg] exclusive per-bucket scan
+    const uint32_t *seg_cnt;   // [nb][nseg] counts (to pick the ranking path)
     const uint32_t *totals;    // [nb]
     uint32_t *qidx;
     uint32_t *qstart;          // [nb + 1]
@@ -89,10 +91,30 @@ struct ScatterParams {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-__device__ __forceinline__ uint32_t rank_below(uint64_t m)
+// orders a wave's LDS accesses across lanes (all lanes of one wave)
+__device__ __forceinline__ void wave_lds_sync()
 {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint64_t lane_lt_mask(uint32_t lane)
+{
+    return lane == 0 ? 0ull : (~0ull >> (64u - lane));
+}
+
+// Lanes (among `valid` ones) whose bucket equals this lane's: ceil(log2 nb)
+// ballots, each keeping the lanes that agree on one bit (match-any emulation).
+__device__ __forceinline__ uint64_t peer_mask(uint32_t bkt, bool valid, uint32_t nb)
+{
+    uint64_t peers = __ballot(valid);
+    const uint32_t kbits = 32u - __builtin_clz(nb - 1u);   // nb >= 2
+    for (uint32_t i = 0; i < kbits; ++i) {
+        const uint64_t bi = __ballot((bkt >> i) & 1u);
+        peers &= ((bkt >> i) & 1u) ? bi : ~bi;
+    }
+    return peers;
 }
 
 __device__ __forceinline__ uint32_t bucket_of(int qv, uint32_t nq)
@@ -322,16 +344,15 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
     }
 
     if (kCount) {
+        // per-bucket counts of this wave segment: lanes sharing a bucket are
+        // found with ceil(log2 nb) ballots (match-any by bit slices); the
+        // lowest lane of each group adds the group size.  Cost is independent
+        // of how many distinct buckets the tile holds.
         const uint32_t bkt = bucket_of(qv, P.nq);
-        uint64_t pending = __ballot(valid);
-        while (pending) {
-            const int leader = __builtin_ctzll(pending);
-            const uint32_t B = __builtin_amdgcn_readlane(bkt, leader);
-            const uint64_t m = __ballot(valid && bkt == B);
-            if (lane == 0)
-                cnt[B] += (uint32_t)__popcll(m);
-            pending &= ~m;
-        }
+        const uint64_t peers = peer_mask(bkt, valid, P.nb);
+        const uint64_t lt = lane_lt_mask(lane);
+        if (valid && (peers & lt) == 0)
+            atomicAdd(&cnt[bkt], (uint32_t)__popcll(peers));
     }
 }
 
@@ -463,6 +484,202 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(const uint32_t *seg_
         totals[b] = run;
 }
 
+// q of a scatter round (slot-major: slot j, lane l -> packet r0 + 64 j + l),
+// clamped into the segment so loads never leave it
+__device__ __forceinline__ void load_round(const int16_t *q, uint32_t r0, uint32_t end,
+                                           uint32_t lane, int32_t (&raw)[kScatterRound])
+{
+#pragma unroll
+    for (int j = 0; j < kScatterRound; ++j)
+        raw[j] = __builtin_nontemporal_load(q + min(r0 + j * kWave + lane, end - 1u));
+}
+
+// Segment feeding at most kFewBuckets buckets (the usual case: nb_procs queues
+// plus the default queue).  The bucket list and each bucket's output cursor
+// live in SGPRs for the whole segment.  Per round and listed bucket u, slot j's
+// ballot(bk == u) is an SGPR mask; a lane's destination is cursor(u) + the
+// count of u below it (mbcnt), so ranking costs ~4 VALU per slot per bucket,
+// needs no LDS, and stores go straight from registers.  q of the next round is
+// in flight while a round is ranked.
+__device__ void scatter_few(const ScatterParams &P, const uint32_t *off, uint32_t gw,
+                            uint32_t beg, uint32_t end, uint32_t lane)
+{
+    uint32_t ub[kFewBuckets], cur[kFewBuckets];
+#pragma unroll
+    for (uint32_t k = 0; k < kFewBuckets; ++k)
+        ub[k] = cur[k] = 0;
+    uint32_t K = 0;
+    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+        const uint32_t b = b0 + lane;
+        uint64_t nz = __ballot(b < P.nb && P.seg_cnt[(size_t)b * P.nseg + gw] != 0);
+        const uint32_t o = b < P.nb ? off[b] : 0u;
+        while (nz) {
+            const uint32_t bit = (uint32_t)__builtin_ctzll(nz);
+            nz &= nz - 1;
+            const uint32_t uu = b0 + bit, oo = __builtin_amdgcn_readlane(o, bit);
+#pragma unroll
+            for (uint32_t k = 0; k < kFewBuckets; ++k)
+                if (k == K) {
+                    ub[k] = uu;
+                    cur[k] = oo;
+                }
+            ++K;
+        }
+    }
+    if (K <= 1) {
+        // the whole segment goes to one list: q need not even be read
+        for (uint32_t i = beg + lane; i < end; i += kWave)
+            __builtin_nontemporal_store(i, P.qidx + cur[0] + (i - beg));
+        return;
+    }
+    constexpr uint32_t kRound = kWave * kScatterRound;
+    int32_t nxt[kScatterRound];
+    load_round(P.q, beg, end, lane, nxt);
+    for (uint32_t r0 = beg; r0 < end; r0 += kRound) {
+        uint32_t bk[kScatterRound];
+        uint64_t vb[kScatterRound];
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j) {
+            // pins the use of the prefetched q here, so the compiler cannot
+            // sink it (and the wait for the load) into the previous round
+            asm volatile("" : "+v"(nxt[j]));
+            bk[j] = bucket_of((int16_t)nxt[j], P.nq);
+            vb[j] = __ballot(r0 + j * kWave + lane < end);
+        }
+        if (r0 + kRound < end)
+            load_round(P.q, r0 + kRound, end, lane, nxt);
+        uint32_t dst[kScatterRound];
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j)
+            dst[j] = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kFewBuckets; ++k) {
+            if (k >= K)
+                break;
+            uint32_t base = cur[k];
+#pragma unroll
+            for (int j = 0; j < kScatterRound; ++j) {
+                const bool hit = bk[j] == ub[k];
+                const uint64_t M = __ballot(hit) & vb[j];
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, base));
+                dst[j] = hit ? r : dst[j];
+                base += (uint32_t)__popcll(M);
+            }
+            cur[k] = base;
+        }
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j)
+            if ((vb[j] >> lane) & 1u)
+                __builtin_nontemporal_store(r0 + j * kWave + lane, P.qidx + dst[j]);
+    }
+}
+
+// General case, any number of buckets, cost independent of nb.  Per 512-packet
+// round:
+//  1) stable rank inside the round.  Per slot, peers (lanes sharing a bucket)
+//     come from bit-sliced ballots; the slot's group leader bumps the round
+//     counter of its bucket with an LDS atomic that returns the count before
+//     it.  A wave's LDS atomics execute in issue order, so issuing all slots
+//     back to back keeps slot order (stability) with a single wait; peers read
+//     their leader's value by ds_bpermute.
+//  2) round-local bucket starts (exclusive scan of the round counts);
+//  3) counting-sort placement into the LDS stage;
+//  4) copy-out: consecutive stage entries of a bucket go to consecutive global
+//     slots, so each store is a few contiguous runs.
+// A full round that is all one bucket (UDP stretches) skips 1)-3).
+__device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t *rc,
+                                uint32_t *rs, uint32_t *stg, uint32_t *stb, uint32_t beg,
+                                uint32_t end, uint32_t lane)
+{
+    constexpr uint32_t kRound = kWave * kScatterRound;
+    const uint64_t lt = lane_lt_mask(lane);
+    for (uint32_t b = lane; b < P.nb; b += kWave)
+        rc[b] = 0;
+    wave_lds_sync();
+    int32_t nxt[kScatterRound];
+    load_round(P.q, beg, end, lane, nxt);
+    for (uint32_t r0 = beg; r0 < end; r0 += kRound) {
+        uint32_t bk[kScatterRound];
+        uint32_t vmask = 0;
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j) {
+            asm volatile("" : "+v"(nxt[j]));
+            bk[j] = bucket_of((int16_t)nxt[j], P.nq);
+            vmask |= (r0 + j * kWave + lane < end ? 1u : 0u) << j;
+        }
+        if (r0 + kRound < end)
+            load_round(P.q, r0 + kRound, end, lane, nxt);
+        const uint32_t B0 = __builtin_amdgcn_readfirstlane(bk[0]);
+        bool same = true;
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j)
+            same &= bk[j] == B0;
+        if (end - r0 >= kRound && __all(same)) {
+            const uint32_t base = __builtin_amdgcn_readfirstlane(off[B0]);
+#pragma unroll
+            for (int j = 0; j < kScatterRound; ++j)
+                __builtin_nontemporal_store(r0 + j * kWave + lane,
+                                            P.qidx + base + j * kWave + lane);
+            wave_lds_sync();
+            if (lane == 0)
+                off[B0] = base + kRound;
+            wave_lds_sync();
+            continue;
+        }
+        // 1)
+        uint64_t peers[kScatterRound];
+        uint32_t before[kScatterRound];
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j)
+            peers[j] = peer_mask(bk[j], (vmask >> j) & 1u, P.nb);
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j) {
+            before[j] = 0;
+            if (((vmask >> j) & 1u) && (peers[j] & lt) == 0)
+                before[j] = atomicAdd(&rc[bk[j]], (uint32_t)__popcll(peers[j]));
+        }
+        uint32_t rank[kScatterRound];
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j) {
+            const int leader = peers[j] ? __builtin_ctzll(peers[j]) : (int)lane;
+            rank[j] = __shfl(before[j], leader, kWave) + (uint32_t)__popcll(peers[j] & lt);
+        }
+        wave_lds_sync();
+        // 2)
+        uint32_t carry = 0;
+        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+            const uint32_t b = b0 + lane;
+            const uint32_t t = b < P.nb ? rc[b] : 0u;
+            const uint32_t x = wave_incl_scan(t, lane);
+            if (b < P.nb)
+                rs[b] = carry + x - t;
+            carry += __shfl(x, kWave - 1, kWave);
+        }
+        wave_lds_sync();
+        // 3)
+#pragma unroll
+        for (int j = 0; j < kScatterRound; ++j)
+            if ((vmask >> j) & 1u) {
+                const uint32_t pos = rs[bk[j]] + rank[j];
+                stg[pos] = r0 + j * kWave + lane;
+                stb[pos] = bk[j];
+            }
+        wave_lds_sync();
+        // 4)
+        for (uint32_t k = lane; k < carry; k += kWave) {
+            const uint32_t b = stb[k];
+            __builtin_nontemporal_store(stg[k], P.qidx + off[b] + (k - rs[b]));
+        }
+        wave_lds_sync();
+        for (uint32_t b = lane; b < P.nb; b += kWave) {
+            off[b] += rc[b];
+            rc[b] = 0;
+        }
+        wave_lds_sync();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Kernel 3: stable scatter of packet indices into per-bucket lists.
 // ---------------------------------------------------------------------------
@@ -471,11 +688,20 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t wave = threadIdx.x / kWave;
     const uint32_t lane = lane_id();
-    uint32_t *off = reinterpret_cast<uint32_t *>(smem) + wave * P.nb;
+    // per wave: off[nb] running output offsets, rc[nb] round counts, rs[nb]
+    // round starts, stg/stb[512] the round's indices/buckets in bucket order
+    uint32_t *wbase = reinterpret_cast<uint32_t *>(smem) +
+                      wave * (3u * P.nb + 2u * kWave * kScatterRound);
+    uint32_t *off = wbase;
+    uint32_t *rc = wbase + P.nb;
+    uint32_t *rs = wbase + 2u * P.nb;
+    uint32_t *stg = wbase + 3u * P.nb;
+    uint32_t *stb = stg + kWave * kScatterRound;
     const uint32_t gw = blockIdx.x * kScatterWaves + wave;
 
-    // start[b] = exclusive scan of totals; off[b] = start[b] + seg_off[gw][b]
-    uint32_t carry = 0;
+    // start[b] = exclusive scan of totals; off[b] = start[b] + seg_off[gw][b];
+    // kseg = buckets this segment feeds
+    uint32_t carry = 0, kseg = 0;
     for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
         const uint32_t b = b0 + lane;
         const uint32_t t = b < P.nb ? P.totals[b] : 0u;
@@ -487,6 +713,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
                 x += y;
         }
         const uint32_t start = carry + x - t;
+        kseg += (uint32_t)__popcll(__ballot(b < P.nb && P.seg_cnt[(size_t)b * P.nseg + gw] != 0));
         if (b < P.nb) {
             off[b] = start + P.seg_off[(size_t)b * P.nseg + gw];
             if (gw == 0)
@@ -503,47 +730,10 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     const uint64_t beg64 = (uint64_t)gw * P.seg;
     const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
     const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
-
-    for (uint32_t r0 = beg; r0 < end; r0 += kWave * kScatterRound) {
-        uint32_t bk[kScatterRound];
-        uint32_t pend = 0;
-#pragma unroll
-        for (int j = 0; j < kScatterRound; ++j) {
-            const uint32_t pkt = r0 + j * kWave + lane;
-            bk[j] = bucket_of(__builtin_nontemporal_load(P.q + min(pkt, end - 1u)), P.nq);
-            pend |= (pkt < end ? 1u : 0u) << j;
-        }
-        for (;;) {
-            const uint64_t act = __ballot(pend != 0u);
-            if (!act)
-                break;
-            const int leader = __builtin_ctzll(act);
-            uint32_t first = 0;
-#pragma unroll
-            for (int j = kScatterRound - 1; j >= 0; --j)
-                first = ((pend >> j) & 1u) ? bk[j] : first;
-            const uint32_t B = __builtin_amdgcn_readlane(first, leader);
-            const uint32_t base = __builtin_amdgcn_readfirstlane(off[B]);
-            uint32_t run = 0;
-#pragma unroll
-            for (int j = 0; j < kScatterRound; ++j) {
-                const bool take = ((pend >> j) & 1u) && bk[j] == B;
-                const uint64_t m = __ballot(take);
-                if (take)
-                    __builtin_nontemporal_store(r0 + j * kWave + lane,
-                                                P.qidx + base + run + rank_below(m));
-                run += (uint32_t)__popcll(m);
-                pend &= ~((take ? 1u : 0u) << j);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0)
-                off[B] = base + run;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-    }
+    if (kseg <= kFewBuckets)
+        scatter_few(P, off, gw, beg, end, lane);
+    else
+        scatter_general(P, off, rc, rs, stg, stb, beg, end, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -885,8 +1075,8 @@ size_t parse_lds(const yrss_ctx *c, bool filter)
 uint32_t grid_for(const yrss_ctx *c, uint32_t n)
 {
     const uint32_t wpb = c->parse_block / kWave;
-    const uint32_t per_block = wpb * kTile;
-    const uint32_t want = (n + per_block - 1) / per_block;
+    const uint64_t per_block = (uint64_t)wpb * kTile;
+    const uint32_t want = (uint32_t)(((uint64_t)n + per_block - 1) / per_block);
     const uint32_t by_lds = (uint32_t)(160u * 1024u / parse_lds(c, true));
     const uint32_t by_waves = std::max(1u, c->waves_per_cu / wpb);
     const uint32_t cap = (uint32_t)c->cus * std::max(1u, std::min(by_lds, by_waves));
@@ -895,10 +1085,10 @@ uint32_t grid_for(const yrss_ctx *c, uint32_t n)
 
 uint32_t seg_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
 {
-    const uint32_t waves = grid * (c->parse_block / kWave);
-    uint32_t s = (n + waves - 1) / waves;
+    const uint64_t waves = (uint64_t)grid * (c->parse_block / kWave);
+    uint64_t s = ((uint64_t)n + waves - 1) / waves;
     s = (s + kTile - 1) / kTile * kTile;
-    return std::max<uint32_t>(s, kTile);
+    return (uint32_t)std::max<uint64_t>(s, kTile);
 }
 
 typedef void (*ParseKernel)(ParseParams);
@@ -1314,7 +1504,7 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     if (!c || !b)
         return -EINVAL;
     const uint32_t n = b->n, win_stride = b->win_stride;
-    if (win_stride < YRSS_WIN_MIN || (win_stride & 15u))
+    if (win_stride < YRSS_WIN_MIN || (win_stride & 15u) || n > YRSS_MAX_BATCH)
         return -EINVAL;
     if (n && (!b->win || !b->len || !b->q))
         return -EINVAL;
@@ -1367,6 +1557,7 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     ScatterParams S;
     S.q = b->q;
     S.seg_off = c->d_seg_off;
+    S.seg_cnt = c->d_seg_cnt;
     S.totals = c->d_totals;
     S.qidx = b->qidx;
     S.qstart = b->qstart;
@@ -1378,7 +1569,9 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     {
         Timed t(c, s, YRSS_K_SCATTER);
         hipLaunchKernelGGL(yrss_scatter, dim3(nseg / kScatterWaves), dim3(kScatterBlock),
-                           (size_t)kScatterWaves * c->nb * sizeof(uint32_t), s, S);
+                           (size_t)kScatterWaves * (3u * c->nb + 2u * kWave * kScatterRound) *
+                               sizeof(uint32_t),
+                           s, S);
     }
     YRSS_HIP(hipGetLastError());
     return 0;
