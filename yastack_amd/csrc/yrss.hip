@@ -48,7 +48,7 @@ constexpr int kScatterBlock = 256;     // 4 waves (segments) per workgroup
 constexpr int kScatterWaves = kScatterBlock / kWave;
 constexpr int kMaxWavesPerCU = 32;
 constexpr int kScatterRound = 8;       // packets per lane per scatter round
-constexpr uint32_t kFewBuckets = 6;    // scatter: distinct-bucket loop up to this many
+constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this many buckets
 constexpr int kTblBytes = 12 * 256 * 4;
 constexpr int kStageBytes = kTile * 64; // 4 KiB per wave
 
@@ -554,49 +554,44 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, uint32_
             dst[j] = 0;
 #pragma unroll
         for (uint32_t k = 0; k < kFewBuckets; ++k) {
-            if (k >= K)
-                break;
-            uint32_t base = cur[k];
+            if (k < K) {
+                uint32_t base = cur[k];
 #pragma unroll
-            for (int j = 0; j < kScatterRound; ++j) {
-                const bool hit = bk[j] == ub[k];
-                const uint64_t M = __ballot(hit) & vb[j];
-                const uint32_t r = __builtin_amdgcn_mbcnt_hi(
-                    (uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, base));
-                dst[j] = hit ? r : dst[j];
-                base += (uint32_t)__popcll(M);
+                for (int j = 0; j < kScatterRound; ++j) {
+                    const bool hit = bk[j] == ub[k];
+                    const uint64_t M = __ballot(hit) & vb[j];
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi(
+                        (uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, base));
+                    dst[j] = hit ? r : dst[j];
+                    base += (uint32_t)__popcll(M);
+                }
+                cur[k] = base;
             }
-            cur[k] = base;
         }
 #pragma unroll
         for (int j = 0; j < kScatterRound; ++j)
-            if ((vb[j] >> lane) & 1u)
-                __builtin_nontemporal_store(r0 + j * kWave + lane, P.qidx + dst[j]);
+            if ((vb[j] >> lane) & 1u) {
+                // plain stores: a store covers a few runs, and L2 merges the
+                // partial lines (non-temporal ones cost 1.6x here)
+                P.qidx[dst[j]] = r0 + j * kWave + lane;
+            }
     }
 }
 
-// General case, any number of buckets, cost independent of nb.  Per 512-packet
-// round:
-//  1) stable rank inside the round.  Per slot, peers (lanes sharing a bucket)
-//     come from bit-sliced ballots; the slot's group leader bumps the round
-//     counter of its bucket with an LDS atomic that returns the count before
-//     it.  A wave's LDS atomics execute in issue order, so issuing all slots
-//     back to back keeps slot order (stability) with a single wait; peers read
-//     their leader's value by ds_bpermute.
-//  2) round-local bucket starts (exclusive scan of the round counts);
-//  3) counting-sort placement into the LDS stage;
-//  4) copy-out: consecutive stage entries of a bucket go to consecutive global
-//     slots, so each store is a few contiguous runs.
-// A full round that is all one bucket (UDP stretches) skips 1)-3).
-__device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t *rc,
-                                uint32_t *rs, uint32_t *stg, uint32_t *stb, uint32_t beg,
+// General case, any number of buckets, cost independent of nb.  off[b] in LDS
+// is bucket b's output cursor for this segment.  Per slot, peers (lanes sharing
+// a bucket) come from bit-sliced ballots; the group's lowest lane bumps the
+// cursor with an LDS atomic whose return value is the group's first output
+// slot.  A wave's LDS atomics execute in issue order, so issuing the slots back
+// to back keeps packet order (FIFO) with one wait; the other lanes read their
+// leader's value by ds_bpermute and add their rank inside the group.  Stores
+// go straight from registers.  A full round that is all one bucket (UDP
+// stretches) skips the ballots.
+__device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t beg,
                                 uint32_t end, uint32_t lane)
 {
     constexpr uint32_t kRound = kWave * kScatterRound;
     const uint64_t lt = lane_lt_mask(lane);
-    for (uint32_t b = lane; b < P.nb; b += kWave)
-        rc[b] = 0;
-    wave_lds_sync();
     int32_t nxt[kScatterRound];
     load_round(P.q, beg, end, lane, nxt);
     for (uint32_t r0 = beg; r0 < end; r0 += kRound) {
@@ -619,62 +614,31 @@ __device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t 
             const uint32_t base = __builtin_amdgcn_readfirstlane(off[B0]);
 #pragma unroll
             for (int j = 0; j < kScatterRound; ++j)
-                __builtin_nontemporal_store(r0 + j * kWave + lane,
-                                            P.qidx + base + j * kWave + lane);
+                P.qidx[base + j * kWave + lane] = r0 + j * kWave + lane;
             wave_lds_sync();
             if (lane == 0)
                 off[B0] = base + kRound;
             wave_lds_sync();
             continue;
         }
-        // 1)
         uint64_t peers[kScatterRound];
-        uint32_t before[kScatterRound];
+        uint32_t first[kScatterRound];
 #pragma unroll
         for (int j = 0; j < kScatterRound; ++j)
             peers[j] = peer_mask(bk[j], (vmask >> j) & 1u, P.nb);
 #pragma unroll
         for (int j = 0; j < kScatterRound; ++j) {
-            before[j] = 0;
+            first[j] = 0;
             if (((vmask >> j) & 1u) && (peers[j] & lt) == 0)
-                before[j] = atomicAdd(&rc[bk[j]], (uint32_t)__popcll(peers[j]));
+                first[j] = atomicAdd(&off[bk[j]], (uint32_t)__popcll(peers[j]));
         }
-        uint32_t rank[kScatterRound];
 #pragma unroll
         for (int j = 0; j < kScatterRound; ++j) {
             const int leader = peers[j] ? __builtin_ctzll(peers[j]) : (int)lane;
-            rank[j] = __shfl(before[j], leader, kWave) + (uint32_t)__popcll(peers[j] & lt);
-        }
-        wave_lds_sync();
-        // 2)
-        uint32_t carry = 0;
-        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-            const uint32_t b = b0 + lane;
-            const uint32_t t = b < P.nb ? rc[b] : 0u;
-            const uint32_t x = wave_incl_scan(t, lane);
-            if (b < P.nb)
-                rs[b] = carry + x - t;
-            carry += __shfl(x, kWave - 1, kWave);
-        }
-        wave_lds_sync();
-        // 3)
-#pragma unroll
-        for (int j = 0; j < kScatterRound; ++j)
-            if ((vmask >> j) & 1u) {
-                const uint32_t pos = rs[bk[j]] + rank[j];
-                stg[pos] = r0 + j * kWave + lane;
-                stb[pos] = bk[j];
-            }
-        wave_lds_sync();
-        // 4)
-        for (uint32_t k = lane; k < carry; k += kWave) {
-            const uint32_t b = stb[k];
-            __builtin_nontemporal_store(stg[k], P.qidx + off[b] + (k - rs[b]));
-        }
-        wave_lds_sync();
-        for (uint32_t b = lane; b < P.nb; b += kWave) {
-            off[b] += rc[b];
-            rc[b] = 0;
+            const uint32_t dst =
+                __shfl(first[j], leader, kWave) + (uint32_t)__popcll(peers[j] & lt);
+            if ((vmask >> j) & 1u)
+                P.qidx[dst] = r0 + j * kWave + lane;
         }
         wave_lds_sync();
     }
@@ -688,15 +652,8 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t wave = threadIdx.x / kWave;
     const uint32_t lane = lane_id();
-    // per wave: off[nb] running output offsets, rc[nb] round counts, rs[nb]
-    // round starts, stg/stb[512] the round's indices/buckets in bucket order
-    uint32_t *wbase = reinterpret_cast<uint32_t *>(smem) +
-                      wave * (3u * P.nb + 2u * kWave * kScatterRound);
-    uint32_t *off = wbase;
-    uint32_t *rc = wbase + P.nb;
-    uint32_t *rs = wbase + 2u * P.nb;
-    uint32_t *stg = wbase + 3u * P.nb;
-    uint32_t *stb = stg + kWave * kScatterRound;
+    // per wave: off[nb], the segment's output cursor per bucket
+    uint32_t *off = reinterpret_cast<uint32_t *>(smem) + wave * P.nb;
     const uint32_t gw = blockIdx.x * kScatterWaves + wave;
 
     // start[b] = exclusive scan of totals; off[b] = start[b] + seg_off[gw][b];
@@ -705,13 +662,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
         const uint32_t b = b0 + lane;
         const uint32_t t = b < P.nb ? P.totals[b] : 0u;
-        uint32_t x = t;
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, kWave);
-            if (lane >= (uint32_t)d)
-                x += y;
-        }
+        const uint32_t x = wave_incl_scan(t, lane);
         const uint32_t start = carry + x - t;
         kseg += (uint32_t)__popcll(__ballot(b < P.nb && P.seg_cnt[(size_t)b * P.nseg + gw] != 0));
         if (b < P.nb) {
@@ -723,9 +674,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     }
     if (gw == 0 && lane == 0)
         P.qstart[P.nb] = carry;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_lds_sync();
 
     const uint64_t beg64 = (uint64_t)gw * P.seg;
     const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
@@ -733,7 +682,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     if (kseg <= kFewBuckets)
         scatter_few(P, off, gw, beg, end, lane);
     else
-        scatter_general(P, off, rc, rs, stg, stb, beg, end, lane);
+        scatter_general(P, off, beg, end, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1569,8 +1518,7 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     {
         Timed t(c, s, YRSS_K_SCATTER);
         hipLaunchKernelGGL(yrss_scatter, dim3(nseg / kScatterWaves), dim3(kScatterBlock),
-                           (size_t)kScatterWaves * (3u * c->nb + 2u * kWave * kScatterRound) *
-                               sizeof(uint32_t),
+                           (size_t)kScatterWaves * c->nb * sizeof(uint32_t),
                            s, S);
     }
     YRSS_HIP(hipGetLastError());
