@@ -47,9 +47,15 @@ constexpr int kTile = 64;              // packets per wave-tile (one per lane)
 constexpr int kScatterBlock = 256;     // 4 waves (segments) per workgroup
 constexpr int kScatterWaves = kScatterBlock / kWave;
 constexpr int kMaxWavesPerCU = 32;
+constexpr uint32_t kMaxChunks = 65536;  // per launch; bounds the count matrix [nb][ncol]
+constexpr uint32_t kCntWords = 512;     // parse: per-wave LDS count slots (chunks x nb)
+constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
 constexpr int kScatterRound = 8;       // packets per lane per scatter round
 constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this many buckets
 constexpr int kTblBytes = 12 * 256 * 4;
+constexpr int kRsrcWord3 = 0x00020000;  // buffer resource dword 3 for gfx9-family (CDNA)
+constexpr uint32_t kOutTiles = 4;       // parse: output burst (tiles buffered in LDS)
+constexpr int kOutBytes = kOutTiles * kTile * (4 + 2 + 1);   // per wave: hash, q, filter
 constexpr int kStageBytes = kTile * 64; // 4 KiB per wave
 
 // Everything yrss_parse_hash needs, passed by value (kernarg segment).
@@ -58,15 +64,19 @@ struct ParseParams {
     const uint16_t *len;
     int16_t *q;
     uint32_t *hash;       // may be null
-    uint32_t *seg_cnt;    // [nb][nseg] bucket-major, or null (no compaction)
+    uint32_t *seg_cnt;    // [nb][ncol] per-chunk counts, bucket-major, or null
     uint32_t n;
     uint32_t stride;
-    uint32_t seg;         // packets per wave segment, multiple of kTile
+    uint32_t seg;         // unused by the parse kernel (scatter group size)
+    uint32_t chunk;       // packets per chunk (dealt round-robin to waves), multiple of kTile
+    uint32_t nchunk;      // chunks in this launch
+    uint32_t ncol;        // row stride of seg_cnt (chunk columns, padded)
+    uint32_t ct_shift;    // tiles per chunk = 2^ct_shift
     uint32_t nq;          // nb_queues
     uint32_t nb;          // buckets = nq + 1 (last = drop)
     uint32_t mod_d;       // divisor: nb_procs or nb_procs-1
     uint32_t q_off;       // 0 or 1 (dispatch_only_core)
-    uint32_t nseg;        // wave segments in this launch
+    uint32_t nseg;        // unused by the parse kernel
     uint64_t mod_m;       // Lemire fastmod constant for mod_d
     int8_t *filter;       // protocol_filter class per packet, or null
     const uint32_t *kni_bm;   // tcp bitmap (2048 words) then udp bitmap (2048 words)
@@ -77,8 +87,7 @@ struct ParseParams {
 
 struct ScatterParams {
     const int16_t *q;
-    const uint32_t *seg_off;   // [nb][nseg] exclusive per-bucket scan
-    const uint32_t *seg_cnt;   // [nb][nseg] counts (to pick the ranking path)
+    const uint32_t *seg_off;   // [nb][ncol] exclusive per-bucket prefix per chunk
     const uint32_t *totals;    // [nb]
     uint32_t *qidx;
     uint32_t *qstart;          // [nb + 1]
@@ -86,7 +95,10 @@ struct ScatterParams {
     uint32_t seg;
     uint32_t nq;
     uint32_t nb;
-    uint32_t nseg;
+    uint32_t nseg;             // groups (one scatter wave each)
+    uint32_t nchunk;           // chunk columns written by the parse kernel
+    uint32_t ncol;             // row stride of seg_off
+    uint32_t gshift;           // a group is 2^gshift chunks
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -213,11 +225,52 @@ __device__ int kni_walk(const ParseParams &P, const uint32_t *kni, const uint32_
     }
 }
 
+// One tile's slot of the wave's output buffer (LDS).
+struct OutSlot {
+    uint16_t *q;
+    uint32_t *h;
+    int8_t *f;
+};
+
+// Writes kOutTiles (or fewer) buffered tiles starting at packet t_first: plain
+// lane-granular stores issued back to back.  Bursts at batch end ran 4-5 %
+// faster than per-tile stores interleaved with the read stream (kernel 200 vs
+// 209 us on one box; tools/hbm_bw.hip "chunk4B-dflt" vs "tile-nt"), and the
+// default policy beat non-temporal (which also evicted q before the scatter
+// re-reads it: scatter 21.6 vs 25.5 us).
+// Buffer resources sized to the valid bytes drop lanes past the end, so every
+// store issues and the vmcnt bookkeeping stays exact.
+template <bool kFilter>
+__device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *oq,
+                                          const uint32_t *oh, const int8_t *of, uint32_t t_first,
+                                          uint32_t ntiles, uint32_t lane)
+{
+    const uint32_t nv = min(ntiles * (uint32_t)kTile, P.n - t_first);
+    const __amdgpu_buffer_rsrc_t rq =
+        __builtin_amdgcn_make_buffer_rsrc(P.q + t_first, 0, (int)(nv * 2u), kRsrcWord3);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
+        P.hash ? (void *)(P.hash + t_first) : (void *)P.q, 0, P.hash ? (int)(nv * 4u) : 0,
+        kRsrcWord3);
+    for (uint32_t j = 0; j < ntiles; ++j) {
+        const uint32_t e = j * kTile + lane;
+        __builtin_amdgcn_raw_buffer_store_b16(oq[e], rq, (int)(e * 2u), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(oh[e], rh, (int)(e * 4u), 0, 0);
+    }
+    if (kFilter) {
+        const __amdgpu_buffer_rsrc_t rf =
+            __builtin_amdgcn_make_buffer_rsrc(P.filter + t_first, 0, (int)nv, kRsrcWord3);
+        for (uint32_t j = 0; j < ntiles; ++j) {
+            const uint32_t e = j * kTile + lane;
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)of[e], rf, (int)e, 0, 0);
+        }
+    }
+}
+
 template <bool kCount, bool kFilter>
 __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_t *tbl,
                                              const uint32_t *kni, u32x4 *stage, uint32_t *cnt,
-                                             uint32_t t0, uint32_t end, uint32_t lane,
-                                             const u32x4 (&r)[4], uint32_t Lraw)
+                                             const OutSlot &ob, uint32_t t0, uint32_t end,
+                                             uint32_t lane, const u32x4 (&r)[4], uint32_t Lraw)
 {
     // Staging layout: chunk c (16 B) of tile packet p at slot p*4 + (c ^ ((p>>2)&3)).
     // Writes: lane l holds chunk l&3 of packet 16k + l/4, so (p>>2)&3 == (l>>4)&3.
@@ -335,13 +388,12 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 
-    if (valid) {
-        P.q[pkt] = (int16_t)qv;
-        if (P.hash)
-            __builtin_nontemporal_store(h, P.hash + pkt);   // never re-read here
-        if (kFilter)
-            P.filter[pkt] = (int8_t)fc;
-    }
+    // outputs go to the wave's LDS out-buffer; flush_out() writes them in
+    // bursts of up to kOutTiles tiles
+    ob.q[lane] = (uint16_t)qv;
+    ob.h[lane] = h;
+    if (kFilter)
+        ob.f[lane] = (int8_t)fc;
 
     if (kCount) {
         // per-bucket counts of this wave segment: lanes sharing a bucket are
@@ -362,8 +414,8 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
 //   kFilter  also classify protocol_filter / KNI (one byte per packet)
 //   kNT      non-temporal (streaming) window loads
 //   kBlock   workgroup size (256/512): waves per CU, one key table per group
-// LDS: key tables 12 KiB | staging 4 KiB per wave | bucket counters per wave |
-//      KNI bitmaps 16 KiB (kFilter only).
+// LDS: key tables 12 KiB | staging 4 KiB per wave | count slots 2 KiB per wave |
+//      output buffer 1.75 KiB per wave | KNI bitmaps 16 KiB (kFilter only).
 // ---------------------------------------------------------------------------
 template <bool kCount, bool kFilter, bool kNT, int kBlock>
 __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
@@ -371,18 +423,21 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     constexpr int kWaves = kBlock / kWave;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint32_t *tbl = reinterpret_cast<uint32_t *>(smem);
-    const uint32_t wave = threadIdx.x / kWave;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t lane = lane_id();
     u32x4 *stage = reinterpret_cast<u32x4 *>(smem + kTblBytes + wave * kStageBytes);
     uint32_t *cnt_base =
         reinterpret_cast<uint32_t *>(smem + kTblBytes + kWaves * kStageBytes);
-    uint32_t *cnt = cnt_base + wave * P.nb;
-    uint32_t *kni = cnt_base + ((kWaves * P.nb + 3u) & ~3u);
+    uint32_t *cnt_w = cnt_base + wave * kCntWords;
+    uint8_t *out_w = reinterpret_cast<uint8_t *>(cnt_base + kWaves * kCntWords) + wave * kOutBytes;
+    uint32_t *oh = reinterpret_cast<uint32_t *>(out_w);
+    uint16_t *oq = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 4);
+    int8_t *of = reinterpret_cast<int8_t *>(out_w + kOutTiles * kTile * 6);
+    uint32_t *kni = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(cnt_base) +
+                                                 kWaves * (kCntWords * 4 + kOutBytes));
 
     const uint32_t gw = blockIdx.x * kWaves + wave;
-    const uint64_t beg64 = (uint64_t)gw * P.seg;
-    const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
-    const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
+    const uint32_t W = gridDim.x * kWaves;
 
     // Byte tables: tbl[j*256+v] = XOR of key windows at bits 8j+b, v's bit b set.
     for (uint32_t e = threadIdx.x; e < 12u * 256u; e += kBlock) {
@@ -397,31 +452,88 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         for (uint32_t e = threadIdx.x; e < (uint32_t)kKniWords; e += kBlock)
             kni[e] = P.kni_enable ? P.kni_bm[e] : 0u;
     if (kCount)
-        for (uint32_t b = lane; b < P.nb; b += kWave)
-            cnt[b] = 0;
+        for (uint32_t e = lane; e < kCntWords; e += kWave)
+            cnt_w[e] = 0;
     __syncthreads();
 
-    for (uint32_t t0 = beg; t0 < end; t0 += kTile) {
-        u32x4 r[4];
-        uint32_t L;
-        load_tile<kNT>(P, t0, end, lane, r, L);
-        process_tile<kCount, kFilter>(P, tbl, kni, stage, cnt, t0, end, lane, r, L);
+    // Chunks are dealt round-robin (chunk c to wave c mod W), so at any moment
+    // the chip reads a compact sliding window of the batch.  One contiguous
+    // segment per wave had 4096 far-apart streams in flight and ran ~10 %
+    // slower on the same box (tools/hbm_bw.hip: pkt_seg vs pkt_chunk).
+    // Each chunk's per-bucket counts accumulate in its own LDS slot and are
+    // stored once, after the last chunk: no global traffic but the windows and
+    // the outputs inside the loop (a per-chunk flush sat in the in-order vmcnt
+    // queue ahead of the next chunk's loads: +13 us on all-TCP).
+    // The wave's tiles form one sequence across its chunks (chunk k is c =
+    // gw + k*W; tile i is tile i mod 2^ct_shift of chunk i >> ct_shift), walked
+    // with one tile of loads in flight ahead of the tile being parsed.  Two
+    // register sets, unrolled by two, so no copy at the latch waits on a load;
+    // the look-ahead load always issues (it re-reads the current tile at the
+    // end) so the wait counts are the same on every path.
+    auto tile_at = [&](uint32_t i, uint32_t &t0, uint32_t &slot) -> bool {
+        const uint32_t kk = i >> P.ct_shift;
+        const uint64_t c = gw + (uint64_t)kk * W;
+        const uint64_t t = c * P.chunk + ((uint64_t)(i & ((1u << P.ct_shift) - 1u)) * kTile);
+        if (c >= P.nchunk || t >= P.n)
+            return false;
+        t0 = (uint32_t)t;
+        slot = kk;
+        return true;
+    };
+    // outputs are buffered per batch of up to kOutTiles consecutive tiles of a
+    // chunk and flushed after its last tile (or the sequence's last)
+    const uint32_t fb_mask = (1u << min(P.ct_shift, 2u)) - 1u;   // kOutTiles = 4
+    auto slot = [&](uint32_t i) {
+        const uint32_t j = (i & fb_mask) * kTile;
+        return OutSlot{oq + j, oh + j, of + j};
+    };
+    auto after = [&](uint32_t i, uint32_t t0, bool last) {
+        if (((i + 1u) & fb_mask) == 0u || last)
+            flush_out<kFilter>(P, oq, oh, of, t0 - (i & fb_mask) * kTile, (i & fb_mask) + 1u,
+                               lane);
+    };
+    uint32_t tA = 0, sA = 0, tB = 0, sB = 0;
+    if (tile_at(0, tA, sA)) {
+        u32x4 rA[4], rB[4];
+        uint32_t LA, LB;
+        load_tile<kNT>(P, tA, P.n, lane, rA, LA);
+        for (uint32_t i = 0;; i += 2) {
+            const bool hB = tile_at(i + 1, tB, sB);
+            load_tile<kNT>(P, hB ? tB : tA, P.n, lane, rB, LB);
+            process_tile<kCount, kFilter>(P, tbl, kni, stage, cnt_w + sA * P.nb, slot(i), tA,
+                                          P.n, lane, rA, LA);
+            after(i, tA, !hB);
+            if (!hB)
+                break;
+            const bool hA = tile_at(i + 2, tA, sA);
+            load_tile<kNT>(P, hA ? tA : tB, P.n, lane, rA, LA);
+            process_tile<kCount, kFilter>(P, tbl, kni, stage, cnt_w + sB * P.nb, slot(i + 1),
+                                          tB, P.n, lane, rB, LB);
+            after(i + 1, tB, !hA);
+            if (!hA)
+                break;
+        }
     }
-
+    const uint32_t k = P.nchunk > gw ? (P.nchunk - gw + W - 1) / W : 0u;   // chunks owned
     if (kCount) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t b = lane; b < P.nb; b += kWave)
-            P.seg_cnt[(size_t)b * P.nseg + gw] = cnt[b];
+        wave_lds_sync();
+        for (uint32_t j = 0; j < k; ++j)
+            for (uint32_t b = lane; b < P.nb; b += kWave)
+                P.seg_cnt[(size_t)b * P.ncol + gw + j * W] = cnt_w[j * P.nb + b];
     }
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 2: per-bucket exclusive scan over wave segments.  One workgroup per
-// bucket; segments <= a few thousand.
+// Kernel 2: per-bucket exclusive scan over the chunk columns, single pass.
+// Workgroup (b, p) scans columns [p*4096, (p+1)*4096) of bucket row b (one
+// uint4 per thread) and chains to its predecessors by decoupled look-back:
+// it publishes its aggregate at once, then sums predecessors' aggregates back
+// to the first inclusive prefix.  Status words carry the launch epoch, so they
+// need no clearing between launches.  The spin is bounded: a look-back that
+// never resolves sets *fault instead of hanging the GPU.
 // ---------------------------------------------------------------------------
 constexpr int kScanBlock = 1024;
+constexpr uint64_t kStFlagP = 1ull << 63;   // status holds the inclusive prefix
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
 {
@@ -434,28 +546,35 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
     return x;
 }
 
-// seg_cnt/seg_off are bucket-major ([nb][nseg]) so one workgroup scans one
-// contiguous row with 16-byte loads; nseg is a multiple of 8.
-__global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(const uint32_t *seg_cnt,
-                                                            uint32_t *seg_off,
-                                                            uint32_t *totals,
-                                                            uint32_t nseg, uint32_t nb)
+struct ScanParams {
+    const uint32_t *cnt;     // [nb][ncol]
+    uint32_t *off;           // [nb][ncol] exclusive prefix per chunk column
+    uint32_t *totals;        // [nb]
+    unsigned long long *status;   // [nb][tiles]: flag | epoch:31 | value:32
+    uint32_t *fault;
+    uint32_t nchunk, ncol, tiles, epoch;
+};
+
+__device__ __forceinline__ unsigned long long scan_status(uint32_t epoch, bool incl, uint32_t v)
+{
+    return (incl ? kStFlagP : 0ull) | ((unsigned long long)(epoch & 0x7fffffffu) << 32) | v;
+}
+
+__global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
 {
     __shared__ uint32_t wsum[kScanBlock / kWave];
-    const uint32_t b = blockIdx.x;
+    __shared__ uint32_t prefix_sh;
+    const uint32_t b = blockIdx.x / P.tiles, p = blockIdx.x % P.tiles;
     const uint32_t lane = lane_id(), wave = threadIdx.x / kWave;
-    const uint32_t nvec = nseg / 4u;                       // uint4 per row
-    const uint32_t per = (nvec + kScanBlock - 1) / kScanBlock;
-    const uint4 *row = reinterpret_cast<const uint4 *>(seg_cnt + (size_t)b * nseg);
-    uint4 *orow = reinterpret_cast<uint4 *>(seg_off + (size_t)b * nseg);
-    uint4 v[2];
-    uint32_t local = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) {
-        const uint32_t i = threadIdx.x * per + k;
-        v[k] = (k < per && i < nvec) ? row[i] : make_uint4(0u, 0u, 0u, 0u);
-        local += v[k].x + v[k].y + v[k].z + v[k].w;
-    }
+    const uint32_t col = p * kScanTile + threadIdx.x * 4u;
+    const uint4 *row = reinterpret_cast<const uint4 *>(P.cnt + (size_t)b * P.ncol);
+    uint4 v = row[col / 4u];
+    // columns past the last chunk were never written this launch
+    if (col + 0u >= P.nchunk) v.x = 0;
+    if (col + 1u >= P.nchunk) v.y = 0;
+    if (col + 2u >= P.nchunk) v.z = 0;
+    if (col + 3u >= P.nchunk) v.w = 0;
+    const uint32_t local = v.x + v.y + v.z + v.w;
     const uint32_t x = wave_incl_scan(local, lane);
     if (lane == kWave - 1)
         wsum[wave] = x;
@@ -465,23 +584,51 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(const uint32_t *seg_
         const uint32_t ws = wave_incl_scan(w, lane);
         if (lane < kScanBlock / kWave)
             wsum[lane] = ws;
-    }
-    __syncthreads();
-    uint32_t run = x - local + (wave ? wsum[wave - 1] : 0u);
-#pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) {
-        const uint32_t i = threadIdx.x * per + k;
-        if (k < per && i < nvec) {
-            uint4 o;
-            o.x = run; run += v[k].x;
-            o.y = run; run += v[k].y;
-            o.z = run; run += v[k].z;
-            o.w = run; run += v[k].w;
-            orow[i] = o;
+        if (lane == kScanBlock / kWave - 1) {
+            // lane 15 holds the tile total: publish, then look back
+            unsigned long long *st = P.status + (size_t)b * P.tiles;
+            const uint32_t total = ws;
+            uint32_t prefix = 0;
+            if (p == 0) {
+                __hip_atomic_store(&st[0], scan_status(P.epoch, true, total), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_store(&st[p], scan_status(P.epoch, false, total), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                uint32_t j = p - 1;
+                uint32_t spins = 0;
+                for (;;) {
+                    const unsigned long long s =
+                        __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((uint32_t)((s >> 32) & 0x7fffffffu) != (P.epoch & 0x7fffffffu)) {
+                        if (++spins > (1u << 22)) {
+                            atomicOr(P.fault, 1u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    prefix += (uint32_t)s;
+                    if ((s & kStFlagP) || j == 0)
+                        break;
+                    --j;
+                }
+                __hip_atomic_store(&st[p], scan_status(P.epoch, true, prefix + total),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            prefix_sh = prefix;
+            if (p == P.tiles - 1)
+                P.totals[b] = prefix + total;
         }
     }
-    if (threadIdx.x == kScanBlock - 1)
-        totals[b] = run;
+    __syncthreads();
+    uint32_t run = prefix_sh + x - local + (wave ? wsum[wave - 1] : 0u);
+    uint4 o;
+    o.x = run; run += v.x;
+    o.y = run; run += v.y;
+    o.z = run; run += v.z;
+    o.w = run;
+    reinterpret_cast<uint4 *>(P.off + (size_t)b * P.ncol)[col / 4u] = o;
 }
 
 // q of a scatter round (slot-major: slot j, lane l -> packet r0 + 64 j + l),
@@ -501,7 +648,7 @@ __device__ __forceinline__ void load_round(const int16_t *q, uint32_t r0, uint32
 // count of u below it (mbcnt), so ranking costs ~4 VALU per slot per bucket,
 // needs no LDS, and stores go straight from registers.  q of the next round is
 // in flight while a round is ranked.
-__device__ void scatter_few(const ScatterParams &P, const uint32_t *off, uint32_t gw,
+__device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const uint32_t *gcnt,
                             uint32_t beg, uint32_t end, uint32_t lane)
 {
     uint32_t ub[kFewBuckets], cur[kFewBuckets];
@@ -511,7 +658,7 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, uint32_
     uint32_t K = 0;
     for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
         const uint32_t b = b0 + lane;
-        uint64_t nz = __ballot(b < P.nb && P.seg_cnt[(size_t)b * P.nseg + gw] != 0);
+        uint64_t nz = __ballot(b < P.nb && gcnt[b] != 0);
         const uint32_t o = b < P.nb ? off[b] : 0u;
         while (nz) {
             const uint32_t bit = (uint32_t)__builtin_ctzll(nz);
@@ -650,23 +797,35 @@ __device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t 
 __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t wave = threadIdx.x / kWave;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t lane = lane_id();
-    // per wave: off[nb], the segment's output cursor per bucket
-    uint32_t *off = reinterpret_cast<uint32_t *>(smem) + wave * P.nb;
+    // per wave: off[nb], the group's output cursor per bucket; gcnt[nb], the
+    // group's packet count per bucket
+    uint32_t *off = reinterpret_cast<uint32_t *>(smem) + wave * 2u * P.nb;
+    uint32_t *gcnt = off + P.nb;
     const uint32_t gw = blockIdx.x * kScatterWaves + wave;
 
-    // start[b] = exclusive scan of totals; off[b] = start[b] + seg_off[gw][b];
-    // kseg = buckets this segment feeds
+    // start[b] = exclusive scan of totals; off[b] = start[b] + the prefix at
+    // the group's first chunk; kseg = buckets this group feeds
+    const uint32_t col = gw << P.gshift, col_end = col + (1u << P.gshift);
     uint32_t carry = 0, kseg = 0;
     for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
         const uint32_t b = b0 + lane;
         const uint32_t t = b < P.nb ? P.totals[b] : 0u;
         const uint32_t x = wave_incl_scan(t, lane);
         const uint32_t start = carry + x - t;
-        kseg += (uint32_t)__popcll(__ballot(b < P.nb && P.seg_cnt[(size_t)b * P.nseg + gw] != 0));
+        uint32_t o = t, oe = t;
         if (b < P.nb) {
-            off[b] = start + P.seg_off[(size_t)b * P.nseg + gw];
+            const uint32_t *row = P.seg_off + (size_t)b * P.ncol;
+            if (col < P.nchunk)
+                o = row[col];
+            if (col_end < P.nchunk)
+                oe = row[col_end];
+        }
+        kseg += (uint32_t)__popcll(__ballot(b < P.nb && oe != o));
+        if (b < P.nb) {
+            off[b] = start + o;
+            gcnt[b] = oe - o;
             if (gw == 0)
                 P.qstart[b] = start;
         }
@@ -680,7 +839,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
     const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
     if (kseg <= kFewBuckets)
-        scatter_few(P, off, gw, beg, end, lane);
+        scatter_few(P, off, gcnt, beg, end, lane);
     else
         scatter_general(P, off, beg, end, lane);
 }
@@ -950,7 +1109,7 @@ struct yrss_ctx {
     // ~64 KiB of loads in flight per CU.
     uint32_t parse_block = 512;  // YRSS_BLOCK: 256 / 512
     bool nt = true;              // YRSS_NT
-    uint32_t waves_per_cu = 16;  // YRSS_WAVES_PER_CU: cap on resident waves
+    uint32_t waves_per_cu = 8;   // YRSS_WAVES_PER_CU: cap on resident waves
     uint32_t nb = 0;
     ParseParams proto{};         // key schedule, modulo constants
     // KNI (protocol_filter) state, ff_dpdk_kni.c:60-61 / ff_dpdk_if.c:103-104
@@ -960,6 +1119,11 @@ struct yrss_ctx {
     uint32_t *d_kni = nullptr;
     // compaction workspace, sized for the largest grid
     uint32_t seg_cap = 0;
+    uint32_t chunk_tiles = 0;       // 0: by bucket count (layout_for())
+    uint32_t group_tiles = 0;       // 0: 64
+    unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
+    uint32_t *d_scan_fault = nullptr;
+    uint32_t scan_epoch = 0;
     uint32_t *d_seg_cnt = nullptr;
     uint32_t *d_seg_off = nullptr;
     uint32_t *d_totals = nullptr;
@@ -1014,8 +1178,7 @@ int hip_fail(const char *what, hipError_t e)
 size_t parse_lds(const yrss_ctx *c, bool filter)
 {
     const size_t w = c->parse_block / kWave;
-    const size_t cnt = (w * c->nb + 3u) & ~(size_t)3u;
-    return kTblBytes + w * kStageBytes + cnt * sizeof(uint32_t) +
+    return kTblBytes + w * kStageBytes + w * (kCntWords * sizeof(uint32_t) + kOutBytes) +
            (filter ? kKniWords * sizeof(uint32_t) : 0u);
 }
 
@@ -1032,12 +1195,43 @@ uint32_t grid_for(const yrss_ctx *c, uint32_t n)
     return std::max(1u, std::min(want, cap));
 }
 
-uint32_t seg_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
+// Work layout of one launch.
+// - chunk (ct tiles): the unit the parse kernel deals round-robin to its waves
+//   and counts per bucket.  Small chunks keep the chip's reads in a compact
+//   window; each wave keeps one LDS count slot per chunk it owns, so
+//   chunks <= waves x (kCntWords / nb), and more buckets get larger chunks.
+// - group (2^shift chunks, >= 64 tiles): one scatter wave.
+// - ncol: chunk columns rounded up to whole scan tiles.
+struct Layout {
+    uint32_t chunk, ct_shift, shift, seg, nchunk, ncol, nseg;
+};
+
+Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
 {
     const uint64_t waves = (uint64_t)grid * (c->parse_block / kWave);
-    uint64_t s = ((uint64_t)n + waves - 1) / waves;
-    s = (s + kTile - 1) / kTile * kTile;
-    return (uint32_t)std::max<uint64_t>(s, kTile);
+    const uint64_t slots = std::max<uint32_t>(1u, kCntWords / c->nb);
+    const uint64_t max_chunks = std::min<uint64_t>(kMaxChunks, waves * slots);
+    const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
+    uint64_t ct = c->chunk_tiles ? c->chunk_tiles : (c->nb <= 17u ? 4u : c->nb <= 65u ? 16u : 64u);
+    ct = std::max<uint64_t>(ct, (tiles + max_chunks - 1) / max_chunks);
+    uint32_t ct_shift = 0;
+    while ((1ull << ct_shift) < ct)
+        ++ct_shift;
+    ct = 1ull << ct_shift;
+    const uint64_t gt = c->group_tiles ? c->group_tiles : 64u;
+    Layout L;
+    L.ct_shift = ct_shift;
+    L.shift = 0;
+    while ((ct << L.shift) < gt)
+        ++L.shift;
+    L.chunk = (uint32_t)(ct * kTile);
+    L.seg = L.chunk << L.shift;
+    L.nchunk = (uint32_t)(((uint64_t)n + L.chunk - 1) / L.chunk);
+    L.ncol = (L.nchunk + kScanTile - 1) / kScanTile * kScanTile;
+    // whole scatter workgroups
+    L.nseg = (uint32_t)((((uint64_t)n + L.seg - 1) / L.seg + kScatterWaves - 1) /
+                        kScatterWaves * kScatterWaves);
+    return L;
 }
 
 typedef void (*ParseKernel)(ParseParams);
@@ -1357,6 +1551,16 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     }
     if (const char *e = getenv("YRSS_NT"))
         c->nt = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_CHUNK_TILES")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 4096)
+            c->chunk_tiles = (uint32_t)v;
+    }
+    if (const char *e = getenv("YRSS_GROUP_TILES")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 65536)
+            c->group_tiles = (uint32_t)v;
+    }
     if (const char *e = getenv("YRSS_WAVES_PER_CU")) {
         const int v = atoi(e);
         if (v >= 4 && v <= kMaxWavesPerCU)
@@ -1371,17 +1575,24 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     c->proto.nq = cfg->nb_queues;
     c->proto.nb = c->nb;
 
-    c->seg_cap = (uint32_t)c->cus * kMaxWavesPerCU;   // >= grid * waves per block
+    c->seg_cap = kMaxChunks;
     const size_t ws = (size_t)c->seg_cap * c->nb * sizeof(uint32_t);
     hipError_t e;
     if ((e = hipMalloc((void **)&c->d_seg_cnt, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_seg_off, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void **)&c->d_scan_status, (size_t)c->nb * (kMaxChunks / kScanTile) *
+                                                       sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMalloc((void **)&c->d_scan_fault, sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMemset(c->d_scan_status, 0, (size_t)c->nb * (kMaxChunks / kScanTile) *
+                                                sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMemset(c->d_scan_fault, 0, sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_kni, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_fault, sizeof(uint32_t))) != hipSuccess ||
         (e = hipHostMalloc((void **)&c->h_fault, sizeof(uint32_t), hipHostMallocDefault)) !=
             hipSuccess ||
         (e = hipMemset(c->d_kni, 0, sizeof(c->kni_bm))) != hipSuccess ||
+        (e = hipMemset(c->d_seg_cnt, 0, ws)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
         yrss_fini(c);
         return hip_fail("yrss_init allocation", e);
@@ -1410,6 +1621,8 @@ void yrss_fini(yrss_ctx *c)
     free_burst(c);
     (void)hipFree(c->d_seg_cnt);
     (void)hipFree(c->d_seg_off);
+    (void)hipFree(c->d_scan_status);
+    (void)hipFree(c->d_scan_fault);
     (void)hipFree(c->d_totals);
     (void)hipFree(c->d_kni);
     (void)hipFree(c->d_fault);
@@ -1472,8 +1685,7 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     }
 
     const uint32_t grid = grid_for(c, n);
-    const uint32_t seg = seg_for(c, n, grid);
-    const uint32_t nseg = grid * (c->parse_block / kWave);   // multiple of kScatterWaves
+    const Layout lay = layout_for(c, n, grid);
 
     ParseParams P = c->proto;
     P.win = b->win;
@@ -1483,8 +1695,12 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     P.seg_cnt = compact ? c->d_seg_cnt : nullptr;
     P.n = n;
     P.stride = win_stride;
-    P.seg = seg;
-    P.nseg = nseg;
+    P.seg = lay.seg;
+    P.nseg = lay.nseg;
+    P.chunk = lay.chunk;
+    P.nchunk = lay.nchunk;
+    P.ncol = lay.ncol;
+    P.ct_shift = lay.ct_shift;
     P.filter = b->filter;
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
@@ -1498,28 +1714,39 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
         return 0;
     {
         Timed t(c, s, YRSS_K_SCAN);
-        hipLaunchKernelGGL(yrss_seg_scan, dim3(c->nb), dim3(kScanBlock), 0, s,
-                           (const uint32_t *)c->d_seg_cnt, c->d_seg_off, c->d_totals,
-                           nseg, c->nb);
+        ScanParams SP;
+        SP.cnt = c->d_seg_cnt;
+        SP.off = c->d_seg_off;
+        SP.totals = c->d_totals;
+        SP.status = c->d_scan_status;
+        SP.fault = c->d_scan_fault;
+        SP.nchunk = lay.nchunk;
+        SP.ncol = lay.ncol;
+        SP.tiles = lay.ncol / kScanTile;
+        if ((++c->scan_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
+            ++c->scan_epoch;
+        SP.epoch = c->scan_epoch;
+        hipLaunchKernelGGL(yrss_seg_scan, dim3(c->nb * SP.tiles), dim3(kScanBlock), 0, s, SP);
     }
     YRSS_HIP(hipGetLastError());
     ScatterParams S;
     S.q = b->q;
     S.seg_off = c->d_seg_off;
-    S.seg_cnt = c->d_seg_cnt;
     S.totals = c->d_totals;
     S.qidx = b->qidx;
     S.qstart = b->qstart;
     S.n = n;
-    S.seg = seg;
+    S.seg = lay.seg;
     S.nq = c->cfg.nb_queues;
     S.nb = c->nb;
-    S.nseg = nseg;
+    S.nseg = lay.nseg;
+    S.nchunk = lay.nchunk;
+    S.ncol = lay.ncol;
+    S.gshift = lay.shift;
     {
         Timed t(c, s, YRSS_K_SCATTER);
-        hipLaunchKernelGGL(yrss_scatter, dim3(nseg / kScatterWaves), dim3(kScatterBlock),
-                           (size_t)kScatterWaves * c->nb * sizeof(uint32_t),
-                           s, S);
+        hipLaunchKernelGGL(yrss_scatter, dim3(lay.nseg / kScatterWaves), dim3(kScatterBlock),
+                           (size_t)kScatterWaves * 2u * c->nb * sizeof(uint32_t), s, S);
     }
     YRSS_HIP(hipGetLastError());
     return 0;
