@@ -2,40 +2,97 @@
 //
 // "Ideal traffic twin" of yrss_parse_hash: moves exactly the same bytes per
 // packet (64-byte window + 2-byte data_len read, 2-byte queue + 4-byte hash
-// written) with perfectly coalesced non-temporal 16-byte loads and no parse
-// work.  Its duration on a given box is the practical floor for the parse
-// kernel's traffic on that box; bench.py reports the parse kernel against it
-// next to the 8 TB/s spec peak, so box-to-box HBM variance is visible.
+// written) in the same access layout as the parse kernel, with no parse work:
+//   - 4-tile chunks dealt round-robin to 8 waves per CU (compact read window);
+//   - each tile's four 16-byte non-temporal loads in flight while the previous
+//     tile is handled (one tile ahead);
+//   - the window reaches its packet's lane through LDS;
+//   - outputs buffered in LDS and written per chunk as one burst of plain
+//     stores.
+// Its duration on a given box is the practical floor for the parse kernel's
+// traffic there; bench.py reports the parse kernel against it next to the
+// 8 TB/s spec peak, so box-to-box HBM variance is visible.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+namespace {
+
+constexpr uint32_t kC = 4;        // tiles per chunk
+constexpr uint32_t kWaves = 8;    // per workgroup (512 threads), one workgroup per CU
+
 __global__ __launch_bounds__(512) void yrss_probe_traffic(const u32x4 *win, const uint16_t *len,
-                                                          int16_t *q, uint32_t *hash,
-                                                          uint32_t nchunks)
+                                                          int16_t *q, uint32_t *hash, uint32_t n)
 {
-    const uint32_t i = blockIdx.x * 512u + threadIdx.x;   // one 16-byte chunk per lane
-    if (i >= nchunks)
-        return;
-    const u32x4 v = __builtin_nontemporal_load(win + i);
-    uint32_t x = v.x ^ v.y ^ v.z ^ v.w;
-    x ^= __shfl_xor(x, 1, 64);
-    x ^= __shfl_xor(x, 2, 64);
-    if ((i & 3u) == 0u) {
-        const uint32_t p = i >> 2;
-        x ^= len[p];
-        q[p] = (int16_t)(x & 0x7fffu);
-        __builtin_nontemporal_store(x, hash + p);
+    __shared__ u32x4 st[kWaves][256];
+    __shared__ uint32_t hb[kWaves][kC * 64];
+    __shared__ uint16_t qb[kWaves][kC * 64];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t W = gridDim.x * kWaves;
+    const uint32_t gw = blockIdx.x * kWaves + w;
+    const uint32_t ntiles = (n + 63u) / 64u;
+    const uint32_t nchunk = (ntiles + kC - 1) / kC;
+    u32x4 nx[4];
+    uint16_t nl = 0;
+    auto issue = [&](uint32_t t0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t p = t0 + 16u * k + (lane >> 2);
+            nx[k] = __builtin_nontemporal_load(win + (size_t)min(p, n - 1u) * 4u + (lane & 3u));
+        }
+        nl = len[min(t0 + lane, n - 1u)];
+    };
+    for (uint32_t c = gw; c < nchunk; c += W) {
+        const uint32_t tb = c * kC, te = min(tb + kC, ntiles);
+        issue(tb * 64u);
+        for (uint32_t t = tb; t < te; ++t) {
+            u32x4 cur[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                cur[k] = nx[k];
+            const uint16_t cl = nl;
+            if (t + 1 < te)
+                issue((t + 1) * 64u);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                st[w][(16u * k + (lane >> 2)) * 4u + (lane & 3u)] = cur[k];
+            __builtin_amdgcn_wave_barrier();
+            const u32x4 a = st[w][lane * 4u + 0], b = st[w][lane * 4u + 1];
+            const u32x4 cc = st[w][lane * 4u + 2], d = st[w][lane * 4u + 3];
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t x = a.x ^ b.y ^ cc.z ^ d.w ^ cl;
+            hb[w][(t - tb) * 64u + lane] = x;
+            qb[w][(t - tb) * 64u + lane] = (uint16_t)(x & 0x7fffu);
+        }
+        const uint32_t base = tb * 64u;
+        for (uint32_t j = 0; j < te - tb; ++j) {
+            const uint32_t e = j * 64u + lane;
+            if (base + e < n) {
+                hash[base + e] = hb[w][e];
+                q[base + e] = (int16_t)qb[w][e];
+            }
+        }
     }
 }
+
+}  // namespace
 
 extern "C" int yrss_probe_traffic_launch(const void *win, const void *len, void *q, void *hash,
                                          uint32_t npkts, void *stream)
 {
-    const uint32_t nchunks = npkts * 4u;
-    hipLaunchKernelGGL(yrss_probe_traffic, dim3((nchunks + 511u) / 512u), dim3(512), 0,
-                       (hipStream_t)stream, (const u32x4 *)win, (const uint16_t *)len,
-                       (int16_t *)q, (uint32_t *)hash, nchunks);
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return -5;
+    }
+    if (npkts == 0)
+        return 0;
+    hipLaunchKernelGGL(yrss_probe_traffic, dim3((unsigned)cus), dim3(512), 0, (hipStream_t)stream,
+                       (const u32x4 *)win, (const uint16_t *)len, (int16_t *)q, (uint32_t *)hash,
+                       npkts);
     return hipGetLastError() == hipSuccess ? 0 : -5;
 }
