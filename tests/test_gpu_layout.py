@@ -1,0 +1,99 @@
+"""Parity across the parse kernel's work layouts (GPU).
+
+The parse kernel deals chunks of tiles round-robin to its waves, counts per
+chunk, and the scatter works per group of chunks (yrss.hip layout_for).  The
+chunk size depends on the bucket count and on the batch size, and can be forced
+with YRSS_CHUNK_TILES / YRSS_GROUP_TILES (read at yrss_init).  Every layout
+must give the same bit-exact q, hash and per-queue FIFO lists as the oracle
+(fs/lib/ff_dpdk_if.c:1945-2113 and the process_packets enqueue order,
+:1058-1094).
+"""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from yastack_amd import SoftRss, abi  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda", 0)
+
+
+def to_np(t, dtype):
+    return t.cpu().numpy().view(dtype)
+
+
+def check(eng, oracle_mod, cfg_tuple, profile, n, stride=64, first=0):
+    npr, nq, soft, only = cfg_tuple
+    win, lens = eng.synth(profile, n, first, stride=stride)
+    res = eng.dispatch_dev(win, lens, stride, n)
+    torch.cuda.synchronize()
+    w_h = win[: n * stride].cpu().numpy()
+    l_h = to_np(lens[:n], np.uint16)
+    c = oracle_mod.cfg(npr, nq, soft, only)
+    q_ref, h_ref = oracle_mod.dispatch_windows(w_h, stride, l_h, c)
+    q = to_np(res.q[:n], np.int16)
+    h = to_np(res.hash[:n], np.uint32)
+    bad = np.nonzero((q != q_ref) | (h != h_ref))[0]
+    assert bad.size == 0, f"{bad.size} q/hash mismatches, first at {bad[:5]}"
+    qi_ref, qs_ref = oracle_mod.process_burst(q_ref, nq)
+    assert np.array_equal(to_np(res.qstart, np.uint32), qs_ref)
+    assert np.array_equal(to_np(res.qidx[:n], np.uint32), qi_ref)
+
+
+class _env:
+    def __init__(self, **kv):
+        self.kv = {k: str(v) for k, v in kv.items()}
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update(self.kv)
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("chunk,group", [(1, 1), (1, 64), (2, 2), (8, 64), (32, 32),
+                                         (4, 256), (128, 128)])
+@pytest.mark.parametrize("profile", [abi.SYN_TCP4, abi.SYN_FUZZ])
+def test_forced_layouts(dev, oracle_mod, chunk, group, profile):
+    """Chunk and group sizes are tuning knobs only: results never change."""
+    cfg = (5, 5, 1, 1)
+    with _env(YRSS_CHUNK_TILES=chunk, YRSS_GROUP_TILES=group):
+        with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            check(eng, oracle_mod, cfg, profile, 300001, first=777)
+
+
+@pytest.mark.parametrize("cfg", [(32, 32, 1, 0), (100, 100, 1, 1), (17, 17, 1, 0)])
+def test_bucket_count_layouts(dev, oracle_mod, cfg):
+    """18..65 buckets get 16-tile chunks, more get 64 (count slots per wave)."""
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        for profile in (abi.SYN_TCP4, abi.SYN_IMIX):
+            check(eng, oracle_mod, cfg, profile, 1 << 20, first=99)
+
+
+@pytest.mark.parametrize("waves", [4, 12, 32])
+def test_occupancy_knob(dev, oracle_mod, waves):
+    """Fewer or more resident waves change the deal (chunks per wave), not results."""
+    cfg = (3, 3, 1, 1)
+    with _env(YRSS_WAVES_PER_CU=waves):
+        with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            check(eng, oracle_mod, cfg, abi.SYN_IMIX, 1 << 21, first=5)
+
+
+def test_batch_beyond_default_chunks(dev, oracle_mod):
+    """2^26 packets: more tiles than 65 536 four-tile chunks, so chunks grow to
+    16 tiles (layout_for); the whole batch is compared with the oracle."""
+    cfg = (3, 3, 1, 1)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        check(eng, oracle_mod, cfg, abi.SYN_TCP4, 1 << 26, first=3)
