@@ -97,3 +97,14 @@ def test_batch_beyond_default_chunks(dev, oracle_mod):
     cfg = (3, 3, 1, 1)
     with SoftRss(*cfg, device=0, max_burst=0) as eng:
         check(eng, oracle_mod, cfg, abi.SYN_TCP4, 1 << 26, first=3)
+
+
+@pytest.mark.parametrize("cfg", [(9, 9, 1, 0), (32, 32, 1, 0), (4096, 256, 1, 1)])
+def test_ballot_scatter_without_ranks(dev, oracle_mod, cfg):
+    """YRSS_NO_RANK=1 keeps many-bucket batches on the ballot-ranked scatter
+    (no per-packet ranks from the parse kernel); same lists either way."""
+    with _env(YRSS_NO_RANK=1):
+        with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            check(eng, oracle_mod, cfg, abi.SYN_FUZZ, 500001, first=11)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        check(eng, oracle_mod, cfg, abi.SYN_FUZZ, 500001, first=11)

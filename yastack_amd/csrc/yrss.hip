@@ -52,10 +52,11 @@ constexpr uint32_t kCntWords = 512;     // parse: per-wave LDS count slots (chun
 constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
 constexpr int kScatterRound = 8;       // packets per lane per scatter round
 constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this many buckets
+constexpr uint32_t kRankStage = 1024;   // ranked scatter: chunk stage (packets) per wave
 constexpr int kTblBytes = 12 * 256 * 4;
 constexpr int kRsrcWord3 = 0x00020000;  // buffer resource dword 3 for gfx9-family (CDNA)
 constexpr uint32_t kOutTiles = 4;       // parse: output burst (tiles buffered in LDS)
-constexpr int kOutBytes = kOutTiles * kTile * (4 + 2 + 1);   // per wave: hash, q, filter
+constexpr int kOutBytes = kOutTiles * kTile * (4 + 2 + 1 + 2);   // hash, q, filter, rank
 constexpr int kStageBytes = kTile * 64; // 4 KiB per wave
 
 // Everything yrss_parse_hash needs, passed by value (kernarg segment).
@@ -65,6 +66,7 @@ struct ParseParams {
     int16_t *q;
     uint32_t *hash;       // may be null
     uint32_t *seg_cnt;    // [nb][ncol] per-chunk counts, bucket-major, or null
+    uint16_t *rank;       // kCount == 2: packet's rank among its chunk's same-bucket packets
     uint32_t n;
     uint32_t stride;
     uint32_t seg;         // unused by the parse kernel (scatter group size)
@@ -99,6 +101,8 @@ struct ScatterParams {
     uint32_t nchunk;           // chunk columns written by the parse kernel
     uint32_t ncol;             // row stride of seg_off
     uint32_t gshift;           // a group is 2^gshift chunks
+    uint32_t chunk;            // packets per chunk
+    const uint16_t *rank;      // ranked mode: rank in chunk per packet (parse kCount == 2)
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -230,6 +234,7 @@ struct OutSlot {
     uint16_t *q;
     uint32_t *h;
     int8_t *f;
+    uint16_t *r;
 };
 
 // Writes kOutTiles (or fewer) buffered tiles starting at packet t_first: plain
@@ -240,9 +245,10 @@ struct OutSlot {
 // re-reads it: scatter 21.6 vs 25.5 us).
 // Buffer resources sized to the valid bytes drop lanes past the end, so every
 // store issues and the vmcnt bookkeeping stays exact.
-template <bool kFilter>
+template <bool kFilter, bool kRank>
 __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *oq,
-                                          const uint32_t *oh, const int8_t *of, uint32_t t_first,
+                                          const uint32_t *oh, const int8_t *of,
+                                          const uint16_t *orank, uint32_t t_first,
                                           uint32_t ntiles, uint32_t lane)
 {
     const uint32_t nv = min(ntiles * (uint32_t)kTile, P.n - t_first);
@@ -264,9 +270,17 @@ __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)of[e], rf, (int)e, 0, 0);
         }
     }
+    if (kRank) {
+        const __amdgpu_buffer_rsrc_t rr =
+            __builtin_amdgcn_make_buffer_rsrc(P.rank + t_first, 0, (int)(nv * 2u), kRsrcWord3);
+        for (uint32_t j = 0; j < ntiles; ++j) {
+            const uint32_t e = j * kTile + lane;
+            __builtin_amdgcn_raw_buffer_store_b16(orank[e], rr, (int)(e * 2u), 0, 0);
+        }
+    }
 }
 
-template <bool kCount, bool kFilter>
+template <int kCount, bool kFilter>
 __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_t *tbl,
                                              const uint32_t *kni, u32x4 *stage, uint32_t *cnt,
                                              const OutSlot &ob, uint32_t t0, uint32_t end,
@@ -396,15 +410,27 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
         ob.f[lane] = (int8_t)fc;
 
     if (kCount) {
-        // per-bucket counts of this wave segment: lanes sharing a bucket are
-        // found with ceil(log2 nb) ballots (match-any by bit slices); the
-        // lowest lane of each group adds the group size.  Cost is independent
-        // of how many distinct buckets the tile holds.
+        // per-bucket counts of this chunk: lanes sharing a bucket are found
+        // with ceil(log2 nb) ballots (match-any by bit slices); the lowest
+        // lane of each group adds the group size.  Cost is independent of how
+        // many distinct buckets the tile holds.  kCount == 2 also keeps each
+        // packet's rank among the chunk's packets of its bucket: the leader's
+        // atomic returns the count before the group (a wave's LDS atomics run
+        // in issue order, so tiles stay in packet order) and each lane adds
+        // its position inside the group.
         const uint32_t bkt = bucket_of(qv, P.nq);
         const uint64_t peers = peer_mask(bkt, valid, P.nb);
         const uint64_t lt = lane_lt_mask(lane);
-        if (valid && (peers & lt) == 0)
+        const bool leader = valid && (peers & lt) == 0;
+        if (kCount == 2) {
+            uint32_t before = 0;
+            if (leader)
+                before = atomicAdd(&cnt[bkt], (uint32_t)__popcll(peers));
+            const int ll = peers ? __builtin_ctzll(peers) : (int)lane;
+            ob.r[lane] = (uint16_t)(__shfl(before, ll, kWave) + (uint32_t)__popcll(peers & lt));
+        } else if (leader) {
             atomicAdd(&cnt[bkt], (uint32_t)__popcll(peers));
+        }
     }
 }
 
@@ -417,7 +443,7 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
 // LDS: key tables 12 KiB | staging 4 KiB per wave | count slots 2 KiB per wave |
 //      output buffer 1.75 KiB per wave | KNI bitmaps 16 KiB (kFilter only).
 // ---------------------------------------------------------------------------
-template <bool kCount, bool kFilter, bool kNT, int kBlock>
+template <int kCount, bool kFilter, bool kNT, int kBlock>
 __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
 {
     constexpr int kWaves = kBlock / kWave;
@@ -433,6 +459,7 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     uint32_t *oh = reinterpret_cast<uint32_t *>(out_w);
     uint16_t *oq = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 4);
     int8_t *of = reinterpret_cast<int8_t *>(out_w + kOutTiles * kTile * 6);
+    uint16_t *orank = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 7);
     uint32_t *kni = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(cnt_base) +
                                                  kWaves * (kCntWords * 4 + kOutBytes));
 
@@ -485,12 +512,12 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     const uint32_t fb_mask = (1u << min(P.ct_shift, 2u)) - 1u;   // kOutTiles = 4
     auto slot = [&](uint32_t i) {
         const uint32_t j = (i & fb_mask) * kTile;
-        return OutSlot{oq + j, oh + j, of + j};
+        return OutSlot{oq + j, oh + j, of + j, orank + j};
     };
     auto after = [&](uint32_t i, uint32_t t0, bool last) {
         if (((i + 1u) & fb_mask) == 0u || last)
-            flush_out<kFilter>(P, oq, oh, of, t0 - (i & fb_mask) * kTile, (i & fb_mask) + 1u,
-                               lane);
+            flush_out<kFilter, kCount == 2>(P, oq, oh, of, orank, t0 - (i & fb_mask) * kTile,
+                                             (i & fb_mask) + 1u, lane);
     };
     uint32_t tA = 0, sA = 0, tB = 0, sB = 0;
     if (tile_at(0, tA, sA)) {
@@ -845,6 +872,103 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
 }
 
 // ---------------------------------------------------------------------------
+// Kernel 3b: scatter with ranks from the parse kernel (many buckets).  Each
+// packet's output slot is start[b] + prefix[b][chunk] + rank: a streaming pass
+// (q and rank read, 2 + 2 B/pkt; index written, 4 B/pkt) whose cost does not
+// depend on the bucket count.  One wave per group of chunks; the chunk's
+// cursors sit in LDS.  Plain stores let L2 merge the scattered 4-byte writes.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterParams P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t lane = lane_id();
+    // per wave: start[nb] list starts; cur[nb] the chunk's global cursor per
+    // bucket; lst[nb] the bucket's first slot in the chunk's sorted stage;
+    // stage[chunk] packet index | bucket << ... (two arrays)
+    uint32_t *wbase = reinterpret_cast<uint32_t *>(smem) +
+                      wave * (3u * P.nb + 2u * kRankStage);
+    uint32_t *start = wbase;
+    uint32_t *cur = start + P.nb;
+    uint32_t *lst = cur + P.nb;
+    uint32_t *sidx = lst + P.nb;
+    uint32_t *sbk = sidx + kRankStage;
+    const uint32_t gw = blockIdx.x * kScatterWaves + wave;
+
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+        const uint32_t b = b0 + lane;
+        const uint32_t t = b < P.nb ? P.totals[b] : 0u;
+        const uint32_t x = wave_incl_scan(t, lane);
+        if (b < P.nb) {
+            start[b] = carry + x - t;
+            if (gw == 0)
+                P.qstart[b] = carry + x - t;
+        }
+        carry += __shfl(x, kWave - 1, kWave);
+    }
+    if (gw == 0 && lane == 0)
+        P.qstart[P.nb] = carry;
+    wave_lds_sync();
+
+    const uint32_t c0 = gw << P.gshift;
+    const uint32_t c1 = min(c0 + (1u << P.gshift), P.nchunk);
+    for (uint32_t c = c0; c < c1; ++c) {
+        // the chunk's cursor per bucket and its counting-sort layout: bucket b
+        // holds stage slots [lst[b], lst[b] + count), count from the prefix
+        // difference to the next chunk
+        uint32_t ls = 0;
+        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+            const uint32_t b = b0 + lane;
+            uint32_t o = 0, cnt = 0;
+            if (b < P.nb) {
+                const uint32_t *row = P.seg_off + (size_t)b * P.ncol;
+                o = row[c];
+                cnt = (c + 1 < P.nchunk ? row[c + 1] : P.totals[b]) - o;
+            }
+            const uint32_t x = wave_incl_scan(cnt, lane);
+            if (b < P.nb) {
+                cur[b] = start[b] + o;
+                lst[b] = ls + x - cnt;
+            }
+            ls += __shfl(x, kWave - 1, kWave);
+        }
+        wave_lds_sync();
+        const uint32_t pb = c * P.chunk;
+        const uint32_t pe = (uint64_t)pb + P.chunk < P.n ? pb + P.chunk : P.n;
+        // place: slot lst[b] + rank
+        for (uint32_t p0 = pb; p0 < pe; p0 += kWave * kScatterRound) {
+            int32_t qv[kScatterRound];
+            uint32_t rv[kScatterRound];
+#pragma unroll
+            for (int j = 0; j < kScatterRound; ++j) {
+                const uint32_t pc = min(p0 + j * kWave + lane, pe - 1u);
+                qv[j] = P.q[pc];
+                rv[j] = P.rank[pc];
+            }
+#pragma unroll
+            for (int j = 0; j < kScatterRound; ++j) {
+                const uint32_t p = p0 + j * kWave + lane;
+                if (p < pe) {
+                    const uint32_t b = bucket_of((int16_t)qv[j], P.nq);
+                    const uint32_t k = lst[b] + rv[j];
+                    sidx[k] = p;
+                    sbk[k] = b;
+                }
+            }
+        }
+        wave_lds_sync();
+        // copy out: a bucket's packets are consecutive in the stage and in
+        // its list, so stores form runs of chunk/nb entries
+        for (uint32_t k = lane; k < pe - pb; k += kWave) {
+            const uint32_t b = sbk[k];
+            P.qidx[cur[b] + (k - lst[b])] = sidx[k];
+        }
+        wave_lds_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // ff_rss_check (ff_dpdk_if.c:1904-1940) in batch: the connect-side RSS check
 // F-Stack runs per candidate lport in in_pcbconnect_setup (in_pcb.c:1131-1170).
 // The tuple is hashed in its raw stored (network-order) byte order, unlike
@@ -1121,6 +1245,9 @@ struct yrss_ctx {
     uint32_t seg_cap = 0;
     uint32_t chunk_tiles = 0;       // 0: by bucket count (layout_for())
     uint32_t group_tiles = 0;       // 0: 64
+    uint16_t *d_rank = nullptr;     // ranked mode workspace (n x u16), grown on demand
+    bool no_rank = false;           // YRSS_NO_RANK: ballot scatter even for many buckets
+    size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
     uint32_t *d_scan_fault = nullptr;
     uint32_t scan_epoch = 0;
@@ -1236,25 +1363,27 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
 
 typedef void (*ParseKernel)(ParseParams);
 
-template <bool C, bool F, bool NT>
+template <int C, bool F, bool NT>
 ParseKernel pick_block(uint32_t block)
 {
     return block == 256 ? yrss_parse_hash<C, F, NT, 256> : yrss_parse_hash<C, F, NT, 512>;
 }
 
-ParseKernel pick_parse(const yrss_ctx *c, bool compact, bool filter)
+template <int C>
+ParseKernel pick_fn(const yrss_ctx *c, bool filter)
 {
-    const int v = (compact ? 4 : 0) | (filter ? 2 : 0) | (c->nt ? 1 : 0);
-    switch (v) {
-    case 0: return pick_block<false, false, false>(c->parse_block);
-    case 1: return pick_block<false, false, true>(c->parse_block);
-    case 2: return pick_block<false, true, false>(c->parse_block);
-    case 3: return pick_block<false, true, true>(c->parse_block);
-    case 4: return pick_block<true, false, false>(c->parse_block);
-    case 5: return pick_block<true, false, true>(c->parse_block);
-    case 6: return pick_block<true, true, false>(c->parse_block);
-    default: return pick_block<true, true, true>(c->parse_block);
-    }
+    if (filter)
+        return c->nt ? pick_block<C, true, true>(c->parse_block)
+                     : pick_block<C, true, false>(c->parse_block);
+    return c->nt ? pick_block<C, false, true>(c->parse_block)
+                 : pick_block<C, false, false>(c->parse_block);
+}
+
+// count: 0 none, 1 per-chunk counts, 2 counts + per-packet chunk ranks
+ParseKernel pick_parse(const yrss_ctx *c, int count, bool filter)
+{
+    return count == 2 ? pick_fn<2>(c, filter) : count == 1 ? pick_fn<1>(c, filter)
+                                                           : pick_fn<0>(c, filter);
 }
 
 hipEvent_t take_event(yrss_ctx *c)
@@ -1556,6 +1685,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         if (v >= 1 && v <= 4096)
             c->chunk_tiles = (uint32_t)v;
     }
+    if (const char *e = getenv("YRSS_NO_RANK"))
+        c->no_rank = atoi(e) != 0;
     if (const char *e = getenv("YRSS_GROUP_TILES")) {
         const int v = atoi(e);
         if (v >= 1 && v <= 65536)
@@ -1622,6 +1753,7 @@ void yrss_fini(yrss_ctx *c)
     (void)hipFree(c->d_seg_cnt);
     (void)hipFree(c->d_seg_off);
     (void)hipFree(c->d_scan_status);
+    (void)hipFree(c->d_rank);
     (void)hipFree(c->d_scan_fault);
     (void)hipFree(c->d_totals);
     (void)hipFree(c->d_kni);
@@ -1686,6 +1818,23 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
 
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
+    // 18..65 buckets (16-tile chunks): the parse kernel also emits each
+    // packet's rank in its chunk and the scatter counting-sorts each chunk in
+    // LDS.  Measured against the ballot scatter on one box: step -4 % at 33
+    // buckets, -2 % at 17; at 10 buckets (256-packet chunks) the ranks' cost in
+    // the parse kernel (+5-8 us) outweighed the gain, and chunks above
+    // kRankStage packets do not fit the stage.
+    const bool ranked = compact && !c->no_rank && c->nb > 17u && lay.chunk <= kRankStage;
+    if (ranked && c->rank_cap < n) {
+        if (c->d_rank) {
+            YRSS_HIP(hipStreamSynchronize(s));
+            (void)hipFree(c->d_rank);
+            c->d_rank = nullptr;
+            c->rank_cap = 0;
+        }
+        YRSS_HIP(hipMalloc((void **)&c->d_rank, (size_t)n * sizeof(uint16_t)));
+        c->rank_cap = n;
+    }
 
     ParseParams P = c->proto;
     P.win = b->win;
@@ -1701,12 +1850,14 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     P.nchunk = lay.nchunk;
     P.ncol = lay.ncol;
     P.ct_shift = lay.ct_shift;
+    P.rank = ranked ? c->d_rank : nullptr;
     P.filter = b->filter;
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
     {
         Timed t(c, s, YRSS_K_PARSE_HASH);
-        hipLaunchKernelGGL(pick_parse(c, compact, filter), dim3(grid), dim3(c->parse_block),
+        hipLaunchKernelGGL(pick_parse(c, ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
+                           dim3(c->parse_block),
                            parse_lds(c, filter), s, P);
     }
     YRSS_HIP(hipGetLastError());
@@ -1743,10 +1894,19 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     S.nchunk = lay.nchunk;
     S.ncol = lay.ncol;
     S.gshift = lay.shift;
+    S.chunk = lay.chunk;
+    S.rank = c->d_rank;
     {
         Timed t(c, s, YRSS_K_SCATTER);
-        hipLaunchKernelGGL(yrss_scatter, dim3(lay.nseg / kScatterWaves), dim3(kScatterBlock),
-                           (size_t)kScatterWaves * 2u * c->nb * sizeof(uint32_t), s, S);
+        if (ranked)
+            hipLaunchKernelGGL(yrss_scatter_ranked, dim3(lay.nseg / kScatterWaves),
+                               dim3(kScatterBlock),
+                               (size_t)kScatterWaves * (3u * c->nb + 2u * kRankStage) *
+                                   sizeof(uint32_t),
+                               s, S);
+        else
+            hipLaunchKernelGGL(yrss_scatter, dim3(lay.nseg / kScatterWaves), dim3(kScatterBlock),
+                               (size_t)kScatterWaves * 2u * c->nb * sizeof(uint32_t), s, S);
     }
     YRSS_HIP(hipGetLastError());
     return 0;
