@@ -344,6 +344,16 @@ int yrss_timing_enable(yrss_ctx *ctx, int kernel_mask);
 int yrss_timing_read(yrss_ctx *ctx, int kernel, double *total_ms,
                      uint32_t *launches);
 
+/* ---- device-side status ----------------------------------------------------------- */
+
+/* Synchronises the device and reports (then clears) a device-side fault of an
+ * earlier yrss_dispatch_dev*: 0 = none, -EIO = the per-queue scan's look-back did not
+ * resolve, so that batch's qidx/qstart are invalid (q and hash are not
+ * affected).  The host-synchronous entry points check this themselves and
+ * return -EIO.  The reference has no equivalent: its per-packet
+ * rte_ring_enqueue cannot fail this way (ff_dpdk_if.c:1087-1093). */
+int yrss_status(yrss_ctx *ctx);
+
 /* ---- introspection --------------------------------------------------------------- */
 
 const char *yrss_version(void);

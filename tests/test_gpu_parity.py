@@ -62,6 +62,7 @@ def run_and_compare(eng, oracle_mod, cfg_tuple, profile, n, stride, first=0, nfl
         qi_ref, qs_ref = oracle_mod.process_burst(q_ref, nq)
         assert np.array_equal(to_np(res.qstart, np.uint32), qs_ref)
         assert np.array_equal(to_np(res.qidx[:n], np.uint32), qi_ref)
+        assert eng.status() == 0
     return q_ref, h_ref
 
 
@@ -317,8 +318,10 @@ def test_timing_hook(dev):
             eng.dispatch_dev(win, lens, 64)
         ms, cnt = eng.timing_read(abi.K_PARSE_HASH)
         assert cnt == 3 and ms > 0
-        ms2, cnt2 = eng.timing_read(abi.K_SCAN)
+        ms2, cnt2 = eng.timing_read(abi.K_SCAN)   # not in the mask
         assert cnt2 == 0
+        ms3, cnt3 = eng.timing_read(abi.K_SCATTER)
+        assert cnt3 == 3 and ms3 > 0
         eng.timing_enable(0)
 
 

@@ -25,7 +25,7 @@ STEPS=${*:-smoke pytest bench prof pmc cbench}
 
 if want smoke; then step smoke 600 python __graft_entry__.py smoke || exit 1; fi
 if want pytest; then
-    step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf
+    step pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
     rc=$?; [ $rc -le 1 ] || exit $rc
 fi
 if want bench; then

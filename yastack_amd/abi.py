@@ -146,6 +146,7 @@ _PROTOS = {
     "yrss_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(_u32)]),
     "yrss_grid_for": (_u32, [_vp, _u32]),
+    "yrss_status": (ctypes.c_int, [_vp]),
     "yrss_set_kni": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
                                     ctypes.c_char_p]),
     "yrss_dispatch_dev_ex": (ctypes.c_int, [_vp, ctypes.POINTER(DevBatch), _vp]),

@@ -25,6 +25,7 @@
 //      order — the stable compaction that stands in for the FIFO
 //      rte_ring_enqueue into dispatch_ring[port][q] (ff_dpdk_if.c:1087-1093).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <errno.h>
 #include <stdint.h>
@@ -629,7 +630,8 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
                         __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if ((uint32_t)((s >> 32) & 0x7fffffffu) != (P.epoch & 0x7fffffffu)) {
                         if (++spins > (1u << 22)) {
-                            atomicOr(P.fault, 1u);
+                            __hip_atomic_store(P.fault, 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
                             break;
                         }
                         __builtin_amdgcn_s_sleep(1);
@@ -701,9 +703,22 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const u
         }
     }
     if (K <= 1) {
-        // the whole segment goes to one list: q need not even be read
-        for (uint32_t i = beg + lane; i < end; i += kWave)
-            __builtin_nontemporal_store(i, P.qidx + cur[0] + (i - beg));
+        // The whole segment goes to one list: q need not even be read, and
+        // the list run is beg, beg+1, ... written as 16-byte stores (1 KiB
+        // per wave-instruction) between an unaligned head and tail.
+        const uint32_t len = end - beg, d = cur[0];
+        const uint32_t head = min(len, (4u - (d & 3u)) & 3u);
+        if (lane < head)
+            P.qidx[d + lane] = beg + lane;
+        const uint32_t nv = (len - head) >> 2;
+        u32x4 *dst = reinterpret_cast<u32x4 *>(P.qidx + d + head);
+        for (uint32_t v = lane; v < nv; v += kWave) {
+            const uint32_t x = beg + head + 4u * v;
+            __builtin_nontemporal_store(u32x4{x, x + 1u, x + 2u, x + 3u}, dst + v);
+        }
+        const uint32_t t = head + 4u * nv + lane;
+        if (t < len)
+            P.qidx[d + t] = beg + t;
         return;
     }
     constexpr uint32_t kRound = kWave * kScatterRound;
@@ -1234,6 +1249,7 @@ struct yrss_ctx {
     uint32_t parse_block = 512;  // YRSS_BLOCK: 256 / 512
     bool nt = true;              // YRSS_NT
     uint32_t waves_per_cu = 8;   // YRSS_WAVES_PER_CU: cap on resident waves
+    unsigned event_flags = hipEventDisableSystemFence;   // YRSS_EVENT_FLAGS
     uint32_t nb = 0;
     ParseParams proto{};         // key schedule, modulo constants
     // KNI (protocol_filter) state, ff_dpdk_kni.c:60-61 / ff_dpdk_if.c:103-104
@@ -1249,7 +1265,7 @@ struct yrss_ctx {
     bool no_rank = false;           // YRSS_NO_RANK: ballot scatter even for many buckets
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
-    uint32_t *d_scan_fault = nullptr;
+    uint32_t *d_scan_fault = nullptr;   // host-coherent pinned word (yrss_status)
     uint32_t scan_epoch = 0;
     uint32_t *d_seg_cnt = nullptr;
     uint32_t *d_seg_off = nullptr;
@@ -1389,8 +1405,11 @@ ParseKernel pick_parse(const yrss_ctx *c, int count, bool filter)
 hipEvent_t take_event(yrss_ctx *c)
 {
     if (c->ev_free.empty()) {
+        // Device-scope release: the outputs are consumed by later kernels on
+        // this device, and the host synchronises on the stream anyway.  The
+        // default system-scope fence writes back L2 at each timed kernel's end.
         hipEvent_t e = nullptr;
-        if (hipEventCreate(&e) != hipSuccess)
+        if (hipEventCreateWithFlags(&e, c->event_flags) != hipSuccess)
             return nullptr;
         return e;
     }
@@ -1399,26 +1418,29 @@ hipEvent_t take_event(yrss_ctx *c)
     return e;
 }
 
+// Per-kernel timing: the events ride on the kernel's own AQL dispatch packet
+// (hipExtLaunchKernel), so timing adds no marker packets to the stream, and
+// they are created with hipEventDisableSystemFence (device-scope release).
+// hipEventRecord markers with the default system-scope fence left ~6 us of
+// idle GPU before and after the timed kernel (profiles/r01_v8_*), ~5 % of a
+// step; with both changes the bench step is within ~1 us of an untimed one.
 struct Timed {
     yrss_ctx *c;
-    hipStream_t s;
     int k;
     hipEvent_t a = nullptr, b = nullptr;
-    Timed(yrss_ctx *c_, hipStream_t s_, int k_) : c(c_), s(s_), k(k_)
+    Timed(yrss_ctx *c_, int k_) : c(c_), k(k_)
     {
         if ((c->timing_mask >> k) & 1u) {
             a = take_event(c);
             b = take_event(c);
-            if (a)
-                (void)hipEventRecord(a, s);
+            if (!a || !b)
+                a = b = nullptr;
         }
     }
     ~Timed()
     {
-        if (a && b) {
-            (void)hipEventRecord(b, s);
+        if (a && b)
             c->ev_pending.push_back({a, b, k});
-        }
     }
 };
 
@@ -1517,6 +1539,15 @@ int ensure_burst(yrss_ctx *c, uint32_t n)
 // Host-staged classification shared by the burst/frames/route entry points.
 // The windows and data_len are already gathered into c->h_win / c->h_len at
 // stride W; results land in the caller's host arrays (NULL = not wanted).
+// A scan look-back that never resolved leaves that batch's lists invalid.
+bool take_scan_fault(yrss_ctx *c)
+{
+    const uint32_t f = __atomic_exchange_n(c->d_scan_fault, 0u, __ATOMIC_ACQ_REL);
+    if (f)
+        fprintf(stderr, "yrss: scan look-back did not resolve; per-queue lists invalid\n");
+    return f != 0;
+}
+
 int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_t *out_hash,
                     uint32_t *out_qidx, uint32_t *out_qstart, int8_t *out_filter)
 {
@@ -1548,6 +1579,8 @@ int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_
                                 hipMemcpyDeviceToHost, s));
     }
     YRSS_HIP(hipStreamSynchronize(s));
+    if (compact && take_scan_fault(c))
+        return -EIO;
     memcpy(out_q, c->h_q, (size_t)n * 2);
     if (out_hash)
         memcpy(out_hash, c->h_hash, (size_t)n * 4);
@@ -1697,6 +1730,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         if (v >= 4 && v <= kMaxWavesPerCU)
             c->waves_per_cu = (uint32_t)v;
     }
+    if (const char *e = getenv("YRSS_EVENT_FLAGS"))   // A/B of the timing-event fence
+        c->event_flags = (unsigned)strtoul(e, nullptr, 0);
     c->nb = (uint32_t)cfg->nb_queues + 1u;
     compute_key_schedule(cfg, c->proto.kwin);
     const bool only = cfg->soft_dispatch && cfg->dispatch_only_core;
@@ -1714,10 +1749,10 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         (e = hipMalloc((void **)&c->d_totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_scan_status, (size_t)c->nb * (kMaxChunks / kScanTile) *
                                                        sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipMalloc((void **)&c->d_scan_fault, sizeof(uint32_t))) != hipSuccess ||
+        (e = hipHostMalloc((void **)&c->d_scan_fault, sizeof(uint32_t),
+                           hipHostMallocCoherent)) != hipSuccess ||
         (e = hipMemset(c->d_scan_status, 0, (size_t)c->nb * (kMaxChunks / kScanTile) *
                                                 sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipMemset(c->d_scan_fault, 0, sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_kni, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_fault, sizeof(uint32_t))) != hipSuccess ||
         (e = hipHostMalloc((void **)&c->h_fault, sizeof(uint32_t), hipHostMallocDefault)) !=
@@ -1728,6 +1763,7 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         yrss_fini(c);
         return hip_fail("yrss_init allocation", e);
     }
+    *c->d_scan_fault = 0;
     if (cfg->max_burst && (rc = ensure_burst(c, cfg->max_burst)) != 0) {
         yrss_fini(c);
         return rc;
@@ -1754,7 +1790,7 @@ void yrss_fini(yrss_ctx *c)
     (void)hipFree(c->d_seg_off);
     (void)hipFree(c->d_scan_status);
     (void)hipFree(c->d_rank);
-    (void)hipFree(c->d_scan_fault);
+    (void)hipHostFree(c->d_scan_fault);
     (void)hipFree(c->d_totals);
     (void)hipFree(c->d_kni);
     (void)hipFree(c->d_fault);
@@ -1855,16 +1891,16 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
     {
-        Timed t(c, s, YRSS_K_PARSE_HASH);
-        hipLaunchKernelGGL(pick_parse(c, ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
-                           dim3(c->parse_block),
-                           parse_lds(c, filter), s, P);
+        Timed t(c, YRSS_K_PARSE_HASH);
+        hipExtLaunchKernelGGL(pick_parse(c, ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
+                              dim3(c->parse_block), (uint32_t)parse_lds(c, filter), s, t.a, t.b,
+                              0, P);
     }
     YRSS_HIP(hipGetLastError());
     if (!compact)
         return 0;
     {
-        Timed t(c, s, YRSS_K_SCAN);
+        Timed t(c, YRSS_K_SCAN);
         ScanParams SP;
         SP.cnt = c->d_seg_cnt;
         SP.off = c->d_seg_off;
@@ -1877,7 +1913,8 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
         if ((++c->scan_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
             ++c->scan_epoch;
         SP.epoch = c->scan_epoch;
-        hipLaunchKernelGGL(yrss_seg_scan, dim3(c->nb * SP.tiles), dim3(kScanBlock), 0, s, SP);
+        hipExtLaunchKernelGGL(yrss_seg_scan, dim3(c->nb * SP.tiles), dim3(kScanBlock), 0, s,
+                              t.a, t.b, 0, SP);
     }
     YRSS_HIP(hipGetLastError());
     ScatterParams S;
@@ -1897,16 +1934,18 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     S.chunk = lay.chunk;
     S.rank = c->d_rank;
     {
-        Timed t(c, s, YRSS_K_SCATTER);
+        Timed t(c, YRSS_K_SCATTER);
         if (ranked)
-            hipLaunchKernelGGL(yrss_scatter_ranked, dim3(lay.nseg / kScatterWaves),
-                               dim3(kScatterBlock),
-                               (size_t)kScatterWaves * (3u * c->nb + 2u * kRankStage) *
-                                   sizeof(uint32_t),
-                               s, S);
+            hipExtLaunchKernelGGL(yrss_scatter_ranked, dim3(lay.nseg / kScatterWaves),
+                                  dim3(kScatterBlock),
+                                  (uint32_t)(kScatterWaves * (3u * c->nb + 2u * kRankStage) *
+                                             sizeof(uint32_t)),
+                                  s, t.a, t.b, 0, S);
         else
-            hipLaunchKernelGGL(yrss_scatter, dim3(lay.nseg / kScatterWaves), dim3(kScatterBlock),
-                               (size_t)kScatterWaves * 2u * c->nb * sizeof(uint32_t), s, S);
+            hipExtLaunchKernelGGL(yrss_scatter, dim3(lay.nseg / kScatterWaves),
+                                  dim3(kScatterBlock),
+                                  (uint32_t)(kScatterWaves * 2u * c->nb * sizeof(uint32_t)), s,
+                                  t.a, t.b, 0, S);
     }
     YRSS_HIP(hipGetLastError());
     return 0;
@@ -2133,6 +2172,8 @@ int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
     YRSS_HIP(hipStreamSynchronize(s));
     if (*c->h_fault)
         return -EFAULT;
+    if (compact && take_scan_fault(c))
+        return -EIO;
     for (int k = 0; k < 4; ++k)
         if (outs[k].user && !outs[k].direct)
             memcpy(outs[k].user, outs[k].stage, outs[k].bytes);
@@ -2332,6 +2373,15 @@ int yrss_synth_dev(yrss_ctx *c, const struct yrss_synth_params *p, uint64_t firs
                        *p, first, n, d_win, win_stride, d_len);
     YRSS_HIP(hipGetLastError());
     return 0;
+}
+
+int yrss_status(yrss_ctx *c)
+{
+    if (!c)
+        return -EINVAL;
+    YRSS_HIP(hipSetDevice(c->device));
+    YRSS_HIP(hipDeviceSynchronize());
+    return take_scan_fault(c) ? -EIO : 0;
 }
 
 int yrss_timing_enable(yrss_ctx *c, int enable)

@@ -278,8 +278,10 @@ class SoftRss:
         return bm
 
     # -- timing hook --------------------------------------------------------
-    def timing_enable(self, on: bool = True) -> None:
-        abi.check(self._lib.yrss_timing_enable(self._ctx, 1 if on else 0), "yrss_timing_enable")
+    def timing_enable(self, mask: int = 1 << abi.K_PARSE_HASH) -> None:
+        """Bracket every launch of kernel k (bit k of mask, abi.K_*) with HIP
+        events on its own dispatch packet; 0 disables."""
+        abi.check(self._lib.yrss_timing_enable(self._ctx, int(mask)), "yrss_timing_enable")
 
     def timing_read(self, kernel: int) -> tuple[float, int]:
         ms = ctypes.c_double()
@@ -287,6 +289,11 @@ class SoftRss:
         abi.check(self._lib.yrss_timing_read(self._ctx, kernel, ctypes.byref(ms),
                                              ctypes.byref(cnt)), "yrss_timing_read")
         return ms.value, cnt.value
+
+    def status(self) -> int:
+        """Synchronise and return (then clear) the device-side fault state:
+        0, or -EIO if the scan's look-back did not resolve (yrss_status)."""
+        return int(self._lib.yrss_status(self._ctx))
 
     def grid_for(self, n: int) -> int:
         return int(self._lib.yrss_grid_for(self._ctx, n))
