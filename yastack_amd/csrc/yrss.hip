@@ -554,13 +554,17 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
 // ---------------------------------------------------------------------------
 // Kernel 2: per-bucket exclusive scan over the chunk columns, single pass.
 // Workgroup (b, p) scans columns [p*4096, (p+1)*4096) of bucket row b (one
-// uint4 per thread) and chains to its predecessors by decoupled look-back:
-// it publishes its aggregate at once, then sums predecessors' aggregates back
-// to the first inclusive prefix.  Status words carry the launch epoch, so they
-// need no clearing between launches.  The spin is bounded: a look-back that
-// never resolves sets *fault instead of hanging the GPU.
+// uint4 per thread), publishes its tile total, and adds the totals of every
+// earlier tile of the row, read at once by one lane each.  All counts exist
+// when the kernel starts (the parse kernel wrote them), so every tile can
+// publish at once and no tile waits on a chain of inclusive prefixes (a
+// serial look-back over 16 tiles was most of this kernel's 5 us).  Status
+// words carry the launch epoch, so they need no clearing between launches.
+// The spin is bounded: a tile total that never appears sets *fault instead of
+// hanging the GPU.
 // ---------------------------------------------------------------------------
 constexpr int kScanBlock = 1024;
+static_assert(kMaxChunks / kScanTile <= kWave, "one look-back lane per scan tile");
 constexpr uint64_t kStFlagP = 1ull << 63;   // status holds the inclusive prefix
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
@@ -612,39 +616,34 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
         const uint32_t ws = wave_incl_scan(w, lane);
         if (lane < kScanBlock / kWave)
             wsum[lane] = ws;
-        if (lane == kScanBlock / kWave - 1) {
-            // lane 15 holds the tile total: publish, then look back
-            unsigned long long *st = P.status + (size_t)b * P.tiles;
-            const uint32_t total = ws;
-            uint32_t prefix = 0;
-            if (p == 0) {
-                __hip_atomic_store(&st[0], scan_status(P.epoch, true, total), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                __hip_atomic_store(&st[p], scan_status(P.epoch, false, total), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                uint32_t j = p - 1;
-                uint32_t spins = 0;
-                for (;;) {
-                    const unsigned long long s =
-                        __hip_atomic_load(&st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((uint32_t)((s >> 32) & 0x7fffffffu) != (P.epoch & 0x7fffffffu)) {
-                        if (++spins > (1u << 22)) {
-                            __hip_atomic_store(P.fault, 1u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    prefix += (uint32_t)s;
-                    if ((s & kStFlagP) || j == 0)
-                        break;
-                    --j;
+        // Lane 15 holds the tile total: publish it, then sum every
+        // predecessor's aggregate at once (one lane per tile, <= 64 tiles per
+        // row), so no tile waits on a chain of inclusive prefixes.
+        unsigned long long *st = P.status + (size_t)b * P.tiles;
+        const uint32_t total = __shfl(ws, kScanBlock / kWave - 1, kWave);
+        if (lane == kScanBlock / kWave - 1)
+            __hip_atomic_store(&st[p], scan_status(P.epoch, false, total), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t mine = 0, spins = 0;
+        bool ready = lane >= p;
+        while (!__all(ready)) {
+            if (!ready) {
+                const unsigned long long w =
+                    __hip_atomic_load(&st[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)((w >> 32) & 0x7fffffffu) == (P.epoch & 0x7fffffffu)) {
+                    mine = (uint32_t)w;
+                    ready = true;
                 }
-                __hip_atomic_store(&st[p], scan_status(P.epoch, true, prefix + total),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            if (++spins > (1u << 22)) {
+                if (lane == 0)
+                    __hip_atomic_store(P.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t prefix = __shfl(wave_incl_scan(mine, lane), kWave - 1, kWave);
+        if (lane == 0) {
             prefix_sh = prefix;
             if (p == P.tiles - 1)
                 P.totals[b] = prefix + total;
