@@ -123,8 +123,9 @@ class Rings:
 @pytest.mark.parametrize("queue_id", [0, 1])
 @pytest.mark.parametrize("kni", [(False, "reject"), (True, "accept"), (True, "reject")])
 @pytest.mark.parametrize("cap", [10**6, 300])
-def test_route_burst_vs_process_packets(oracle_mod, queue_id, kni, cap):
-    n, nq = 3000, 4
+@pytest.mark.parametrize("n", [3000, 6000])   # one-launch small path / multi-kernel path
+def test_route_burst_vs_process_packets(oracle_mod, queue_id, kni, cap, n):
+    nq = 4
     win, lens = oracle_mod.synth(abi.SYN_FUZZ, n, 5, stride=80)
     frames = []
     for i in range(n):

@@ -1127,56 +1127,90 @@ __device__ __forceinline__ uint32_t quad_word(const u32x4 &hv, uint32_t lane, ui
     return __shfl(pick_word(hv, (o >> 2) & 3u), (int)((lane & ~3u) | (o >> 4)), kWave);
 }
 
-__global__ __launch_bounds__(256) void yrss_gather_zc(GatherParams G)
+// Windows of the calling wave's packets (4 lanes per packet, 16 packets per
+// wave-iteration): the mbuf header (or the frame pointer/length pair) and the
+// first 80 bytes of data, read from registered host memory, into G.win at
+// stride 80 and G.len.  kB iterations run in lockstep phases (pointers, then
+// headers, then data), so a wave has kB x 16 packets' PCIe reads in flight
+// per dependent step instead of 16.
+template <int kB>
+__device__ __forceinline__ void gather_quads(const GatherParams &G, uint32_t wave,
+                                             uint32_t nwaves, uint32_t lane)
 {
-    const uint32_t lane = lane_id(), c = lane & 3u;
-    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) / kWave;
-    const uint32_t nwaves = gridDim.x * (256u / kWave);
-    for (uint32_t p0 = wave * 16u; p0 < G.n; p0 += nwaves * 16u) {
-        const uint32_t i = p0 + (lane >> 2);
-        const bool valid = i < G.n;
-        const uint64_t m = valid ? G.ptrs[i] : 0u;
-        uint64_t data;
-        uint32_t L;
-        bool ok_m;
+    const uint32_t c = lane & 3u;
+    for (uint32_t p0 = wave * 16u * kB; p0 < G.n; p0 += nwaves * 16u * kB) {
+        uint32_t idx[kB], L[kB];
+        uint64_t m[kB], data[kB];
+        bool ok_m[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            idx[k] = p0 + 16u * k + (lane >> 2);
+            m[k] = idx[k] < G.n ? G.ptrs[idx[k]] : 0u;
+            L[k] = (G.frames && idx[k] < G.n) ? G.lens[idx[k]] : 0u;
+        }
         if (G.frames) {
             // frames mode: the host already knows data pointer and data_len
-            data = m;
-            L = valid ? G.lens[i] : 0u;
-            ok_m = valid;
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+                data[k] = m[k];
+                ok_m[k] = idx[k] < G.n;
+            }
         } else {
-            int64_t dm = 0;
-            ok_m = valid && host_xlate(G, m, 64u, &dm);
-            u32x4 hv = {0u, 0u, 0u, 0u};
-            if (ok_m)
-                hv = host_load16(m + dm + 16u * c);
+            u32x4 hv[kB];
+            int64_t dm[kB];
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+                dm[k] = 0;
+                ok_m[k] = idx[k] < G.n && host_xlate(G, m[k], 64u, &dm[k]);
+                hv[k] = u32x4{0u, 0u, 0u, 0u};
+                if (ok_m[k])
+                    hv[k] = host_load16(m[k] + dm[k] + 16u * c);
+            }
             const uint32_t ob = G.off_buf_addr, od = G.off_data_off, ol = G.off_data_len;
-            const uint64_t buf = (uint64_t)quad_word(hv, lane, ob) |
-                                 ((uint64_t)quad_word(hv, lane, ob + 4u) << 32);
-            const uint32_t doff = (quad_word(hv, lane, od & ~3u) >> (8u * (od & 3u))) & 0xffffu;
-            L = (quad_word(hv, lane, ol & ~3u) >> (8u * (ol & 3u))) & 0xffffu;
-            data = buf + doff;
+#pragma unroll
+            for (int k = 0; k < kB; ++k) {
+                const uint64_t buf = (uint64_t)quad_word(hv[k], lane, ob) |
+                                     ((uint64_t)quad_word(hv[k], lane, ob + 4u) << 32);
+                const uint32_t doff =
+                    (quad_word(hv[k], lane, od & ~3u) >> (8u * (od & 3u))) & 0xffffu;
+                L[k] = (quad_word(hv[k], lane, ol & ~3u) >> (8u * (ol & 3u))) & 0xffffu;
+                data[k] = buf + doff;
+            }
         }
-        const uint32_t need = (min(L, (uint32_t)YRSS_WIN_FULL) + 15u) & ~15u;   // bytes to read
-        int64_t dd = 0;
-        const bool ok_d = ok_m && (need == 0 || host_xlate(G, data, need, &dd));
-        uint8_t *dst = G.win + (size_t)i * YRSS_WIN_FULL;
-        if (valid) {
-            u32x4 w = {0u, 0u, 0u, 0u};
-            if (ok_d && 16u * c < need)
-                w = host_load16(data + dd + 16u * c);
-            *reinterpret_cast<u32x4 *>(dst + 16u * c) = w;
+        u32x4 w[kB], t[kB];
+        bool ok_d[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const uint32_t need = (min(L[k], (uint32_t)YRSS_WIN_FULL) + 15u) & ~15u;
+            int64_t dd = 0;
+            ok_d[k] = ok_m[k] && (need == 0 || host_xlate(G, data[k], need, &dd));
+            w[k] = u32x4{0u, 0u, 0u, 0u};
+            t[k] = u32x4{0u, 0u, 0u, 0u};
+            if (ok_d[k] && 16u * c < need)
+                w[k] = host_load16(data[k] + dd + 16u * c);
+            if (ok_d[k] && c == 0 && need > 64u)
+                t[k] = host_load16(data[k] + dd + 64u);
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            if (idx[k] >= G.n)
+                continue;
+            uint8_t *dst = G.win + (size_t)idx[k] * YRSS_WIN_FULL;
+            *reinterpret_cast<u32x4 *>(dst + 16u * c) = w[k];
             if (c == 0) {
-                u32x4 t = {0u, 0u, 0u, 0u};
-                if (ok_d && need > 64u)
-                    t = host_load16(data + dd + 64u);
-                *reinterpret_cast<u32x4 *>(dst + 64u) = t;
-                G.len[i] = (uint16_t)L;
-                if (!ok_d)
-                    atomicOr(G.fault, 1u);
+                *reinterpret_cast<u32x4 *>(dst + 64u) = t[k];
+                G.len[idx[k]] = (uint16_t)L[k];
+                if (!ok_d[k])   // plain store: the word may live in host memory
+                    __hip_atomic_store(G.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
     }
+}
+
+__global__ __launch_bounds__(256) void yrss_gather_zc(GatherParams G)
+{
+    const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) / kWave;
+    gather_quads<1>(G, wave, gridDim.x * (256u / kWave), lane_id());
 }
 
 // hash.rss write-back straight into the host mbufs (YRSS_F_WRITE_RSS)
@@ -1189,6 +1223,158 @@ __global__ __launch_bounds__(256) void yrss_writeback_zc(GatherParams G)
     int64_t dm = 0;
     if (host_xlate(G, m, G.off_hash_rss + 4u, &dm))
         *reinterpret_cast<uint32_t *>(m + dm + G.off_hash_rss) = G.hash[i];
+}
+
+// ---------------------------------------------------------------------------
+// Small host bursts (n <= 4096, nb <= 64) in ONE launch of ONE workgroup.
+// The host-resident entry points at F-Stack's burst sizes (32 at
+// ff_dpdk_if.c:83, 1024 in BASELINE) were bound by per-call HIP overhead:
+// memset + gather + parse + scan + scatter + four D2H copies = ten queue
+// operations, 39-62 us a burst.  Here 16 waves do everything:
+//   gather   (zero-copy modes) mbuf headers and windows from registered host
+//            memory into device scratch (gather_quads, each wave its own
+//            tiles, pointer / header / data reads in lockstep rounds);
+//   parse    each wave loads all its (up to four) 64-packet tiles, then runs
+//            them through the same process_tile() as yrss_parse_hash
+//            (per-tile bucket counts and per-packet ranks in LDS, outputs
+//            kept in the wave's LDS buffer);
+//   lists    per-bucket prefix over the tiles in LDS, then every packet's
+//            list slot = start[b] + prefix[tile][b] + rank: the same stable
+//            FIFO lists as parse + scan + scatter;
+//   outputs  straight into host-visible memory (the caller's registered
+//            arrays or the context's pinned staging), so no copy follows.
+// A multi-workgroup variant (one tile per wave, last-arriver ticket for the
+// lists) was slower at every burst size measured: 21 vs 16 us at 32 packets,
+// 34 vs 33 at 1024 (profiles/r01_v11_small_burst.log).
+// ---------------------------------------------------------------------------
+constexpr int kSmallBlock = 1024;
+constexpr uint32_t kSmallWaves = kSmallBlock / kWave;          // 16
+constexpr uint32_t kSmallTiles = kSmallWaves * kOutTiles;      // 64
+constexpr uint32_t kSmallMaxPkts = kSmallTiles * kTile;        // 4096
+constexpr uint32_t kSmallMaxNb = kWave;                        // one lane per bucket
+
+struct SmallParams {
+    ParseParams P;       // win/len: windows to parse; q/hash/filter: host-visible outputs
+    GatherParams G;      // gather: source pointers; G.win/G.len = P.win/P.len (scratch)
+    uint32_t *qidx;      // host-visible, or null
+    uint32_t *qstart;    // host-visible [nb + 1], or null
+    uint32_t gather;     // 1: gather the windows first (zero-copy modes)
+    uint32_t writeback;  // 1: store hash.rss into each mbuf (YRSS_F_WRITE_RSS)
+};
+
+size_t small_lds(uint32_t nb, bool filter)
+{
+    return kTblBytes + kSmallWaves * (kStageBytes + kOutBytes) +
+           (size_t)(kSmallTiles * nb + kSmallMaxNb) * sizeof(uint32_t) +
+           (filter ? kKniWords * sizeof(uint32_t) : 0u);
+}
+
+template <bool kFilter>
+__global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
+{
+    const ParseParams &P = S.P;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t lane = lane_id();
+    uint32_t *tbl = reinterpret_cast<uint32_t *>(smem);
+    u32x4 *stage = reinterpret_cast<u32x4 *>(smem + kTblBytes + wave * kStageBytes);
+    uint8_t *out_w = smem + kTblBytes + kSmallWaves * kStageBytes + wave * kOutBytes;
+    uint32_t *oh = reinterpret_cast<uint32_t *>(out_w);
+    uint16_t *oq = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 4);
+    int8_t *of = reinterpret_cast<int8_t *>(out_w + kOutTiles * kTile * 6);
+    uint16_t *orank = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 7);
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + kTblBytes +
+                                                 kSmallWaves * (kStageBytes + kOutBytes));
+    uint32_t *start = cnt + kSmallTiles * P.nb;
+    uint32_t *kni = start + kSmallMaxNb;
+
+    // wave w owns tiles w, w + 16, w + 32, w + 48: with 4 lockstep rounds of
+    // 16 packets, gather_quads' wave-iteration p0 = 64 (w + 16 j) is tile j's
+    if (S.gather)
+        gather_quads<4>(S.G, wave, kSmallWaves, lane);
+    for (uint32_t e = threadIdx.x; e < 12u * 256u; e += kSmallBlock) {
+        const uint32_t jt = e >> 8, v = e & 255u;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b)
+            acc ^= (v & (0x80u >> b)) ? P.kwin[8 * jt + b] : 0u;
+        tbl[e] = acc;
+    }
+    if (kFilter)
+        for (uint32_t e = threadIdx.x; e < (uint32_t)kKniWords; e += kSmallBlock)
+            kni[e] = P.kni_enable ? P.kni_bm[e] : 0u;
+    for (uint32_t e = threadIdx.x; e < kSmallTiles * P.nb; e += kSmallBlock)
+        cnt[e] = 0;
+    // also orders the gathered windows (global scratch written by this
+    // workgroup) before the parse reads them
+    __syncthreads();
+
+    const uint32_t ntiles = (P.n + kTile - 1) / kTile;
+    // all of the wave's tiles are loaded before the first is parsed: the
+    // windows may sit in host memory, one PCIe round trip for all of them
+    u32x4 r[kOutTiles][4];
+    uint32_t L[kOutTiles];
+#pragma unroll
+    for (uint32_t j = 0; j < kOutTiles; ++j) {
+        const uint32_t t = min(wave + j * kSmallWaves, ntiles - 1u);
+        load_tile<false>(P, t * kTile, P.n, lane, r[j], L[j]);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kOutTiles; ++j) {
+        const uint32_t t = wave + j * kSmallWaves;
+        if (t >= ntiles)
+            break;
+        process_tile<2, kFilter>(P, tbl, kni, stage, cnt + t * P.nb,
+                                 OutSlot{oq + j * kTile, oh + j * kTile, of + j * kTile,
+                                         orank + j * kTile},
+                                 t * kTile, P.n, lane, r[j], L[j]);
+    }
+    __syncthreads();
+    // per bucket: exclusive prefix over the tiles (in place) and the total
+    if (threadIdx.x < P.nb) {
+        const uint32_t b = threadIdx.x;
+        uint32_t run = 0;
+        for (uint32_t t = 0; t < ntiles; ++t) {
+            const uint32_t v = cnt[t * P.nb + b];
+            cnt[t * P.nb + b] = run;
+            run += v;
+        }
+        start[b] = run;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const uint32_t tot = lane < P.nb ? start[lane] : 0u;
+        const uint32_t x = wave_incl_scan(tot, lane);
+        if (lane < P.nb) {
+            start[lane] = x - tot;
+            if (S.qstart)
+                S.qstart[lane] = x - tot;
+        }
+        if (lane == kWave - 1 && S.qstart)
+            S.qstart[P.nb] = x;
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < kOutTiles; ++j) {
+        const uint32_t t = wave + j * kSmallWaves;
+        if (t >= ntiles)
+            break;
+        flush_out<kFilter, false>(P, oq + j * kTile, oh + j * kTile, of + j * kTile,
+                                  orank + j * kTile, t * kTile, 1u, lane);
+        const uint32_t pkt = t * kTile + lane;
+        if (pkt < P.n) {
+            if (S.qidx) {
+                const uint32_t b = bucket_of((int16_t)oq[j * kTile + lane], P.nq);
+                S.qidx[start[b] + cnt[t * P.nb + b] + orank[j * kTile + lane]] = pkt;
+            }
+            if (S.writeback) {
+                const uint64_t m = S.G.ptrs[pkt];
+                int64_t dm = 0;
+                if (host_xlate(S.G, m, S.G.off_hash_rss + 4u, &dm))
+                    *reinterpret_cast<uint32_t *>(m + dm + S.G.off_hash_rss) =
+                        oh[j * kTile + lane];
+            }
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1293,7 +1479,19 @@ struct yrss_ctx {
     uint64_t *h_ptrs = nullptr;
     uint64_t *d_ptrs = nullptr;
     uint32_t *d_fault = nullptr;
-    uint32_t *h_fault = nullptr;
+    uint32_t *h_fault = nullptr;    // host-coherent
+    // device views of the pinned staging: the small-burst kernel reads and
+    // writes it in place (no copies)
+    bool no_small = false;          // YRSS_NO_SMALL: always the multi-kernel path
+    uint8_t *dh_win = nullptr;
+    uint16_t *dh_len = nullptr;
+    int16_t *dh_q = nullptr;
+    uint32_t *dh_hash = nullptr;
+    uint32_t *dh_qidx = nullptr;
+    uint32_t *dh_qstart = nullptr;
+    int8_t *dh_filter = nullptr;
+    uint64_t *dh_ptrs = nullptr;
+    uint32_t *dh_fault = nullptr;
     // timing
     uint32_t timing_mask = 0;    // bit k: bracket kernel k with events
     std::vector<hipEvent_t> ev_free;
@@ -1531,6 +1729,14 @@ int ensure_burst(yrss_ctx *c, uint32_t n)
     YRSS_HIP(hipMalloc((void **)&c->d_filter, (size_t)cap));
     YRSS_HIP(hipHostMalloc((void **)&c->h_ptrs, (size_t)cap * 8, hipHostMallocDefault));
     YRSS_HIP(hipMalloc((void **)&c->d_ptrs, (size_t)cap * 8));
+    YRSS_HIP(hipHostGetDevicePointer((void **)&c->dh_win, c->h_win, 0));
+    YRSS_HIP(hipHostGetDevicePointer((void **)&c->dh_len, c->h_len, 0));
+    YRSS_HIP(hipHostGetDevicePointer((void **)&c->dh_q, c->h_q, 0));
+    YRSS_HIP(hipHostGetDevicePointer((void **)&c->dh_hash, c->h_hash, 0));
+    YRSS_HIP(hipHostGetDevicePointer((void **)&c->dh_qidx, c->h_qidx, 0));
+    YRSS_HIP(hipHostGetDevicePointer((void **)&c->dh_qstart, c->h_qstart, 0));
+    YRSS_HIP(hipHostGetDevicePointer((void **)&c->dh_filter, c->h_filter, 0));
+    YRSS_HIP(hipHostGetDevicePointer((void **)&c->dh_ptrs, c->h_ptrs, 0));
     c->burst_cap = cap;
     return 0;
 }
@@ -1547,11 +1753,70 @@ bool take_scan_fault(yrss_ctx *c)
     return f != 0;
 }
 
+bool small_ok(const yrss_ctx *c, uint32_t n)
+{
+    return !c->no_small && n >= 1 && n <= kSmallMaxPkts && c->nb <= kSmallMaxNb;
+}
+
+// One launch of yrss_burst_small on the context stream.  S.P.win/len and the
+// output pointers are filled by the caller; this adds the configuration.
+int small_launch(yrss_ctx *c, SmallParams &S, bool filter)
+{
+    const ParseParams &proto = c->proto;
+    ParseParams &P = S.P;
+    memcpy(P.kwin, proto.kwin, sizeof(P.kwin));
+    P.nq = proto.nq;
+    P.nb = proto.nb;
+    P.mod_d = proto.mod_d;
+    P.q_off = proto.q_off;
+    P.mod_m = proto.mod_m;
+    P.seg_cnt = nullptr;
+    P.rank = nullptr;
+    P.kni_bm = c->d_kni;
+    P.kni_enable = c->kni_enable ? 1u : 0u;
+    const size_t lds = small_lds(c->nb, filter);
+    const dim3 grid(1);
+    if (filter)
+        hipLaunchKernelGGL(yrss_burst_small<true>, grid, dim3(kSmallBlock), lds, c->stream, S);
+    else
+        hipLaunchKernelGGL(yrss_burst_small<false>, grid, dim3(kSmallBlock), lds, c->stream, S);
+    YRSS_HIP(hipGetLastError());
+    return 0;
+}
+
 int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_t *out_hash,
                     uint32_t *out_qidx, uint32_t *out_qstart, int8_t *out_filter)
 {
     hipStream_t s = c->stream;
     const bool compact = out_qidx && out_qstart;
+    if (small_ok(c, n)) {
+        // the kernel reads the staged windows and writes the staging in place
+        SmallParams S;
+        memset(&S, 0, sizeof(S));
+        S.P.win = c->dh_win;
+        S.P.len = c->dh_len;
+        S.P.stride = W;
+        S.P.n = n;
+        S.P.q = c->dh_q;
+        S.P.hash = out_hash ? c->dh_hash : nullptr;
+        S.P.filter = out_filter ? c->dh_filter : nullptr;
+        S.qidx = compact ? c->dh_qidx : nullptr;
+        S.qstart = compact ? c->dh_qstart : nullptr;
+        int rc = small_launch(c, S, out_filter != nullptr);
+        if (rc)
+            return rc;
+        YRSS_HIP(hipStreamSynchronize(s));
+        memcpy(out_q, c->h_q, (size_t)n * 2);
+        if (out_hash)
+            memcpy(out_hash, c->h_hash, (size_t)n * 4);
+        if (out_filter)
+            memcpy(out_filter, c->h_filter, n);
+        if (compact) {
+            memcpy(out_qidx, c->h_qidx, (size_t)n * 4);
+            memcpy(out_qstart, c->h_qstart, (c->nb + 1) * 4);
+        }
+        return 0;
+    }
     YRSS_HIP(hipMemcpyAsync(c->d_win, c->h_win, (size_t)n * W, hipMemcpyHostToDevice, s));
     YRSS_HIP(hipMemcpyAsync(c->d_len, c->h_len, (size_t)n * 2, hipMemcpyHostToDevice, s));
     yrss_dev_batch b;
@@ -1729,6 +1994,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         if (v >= 4 && v <= kMaxWavesPerCU)
             c->waves_per_cu = (uint32_t)v;
     }
+    if (const char *e = getenv("YRSS_NO_SMALL"))
+        c->no_small = atoi(e) != 0;
     if (const char *e = getenv("YRSS_EVENT_FLAGS"))   // A/B of the timing-event fence
         c->event_flags = (unsigned)strtoul(e, nullptr, 0);
     c->nb = (uint32_t)cfg->nb_queues + 1u;
@@ -1754,8 +2021,9 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
                                                 sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_kni, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_fault, sizeof(uint32_t))) != hipSuccess ||
-        (e = hipHostMalloc((void **)&c->h_fault, sizeof(uint32_t), hipHostMallocDefault)) !=
+        (e = hipHostMalloc((void **)&c->h_fault, sizeof(uint32_t), hipHostMallocCoherent)) !=
             hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&c->dh_fault, c->h_fault, 0)) != hipSuccess ||
         (e = hipMemset(c->d_kni, 0, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipMemset(c->d_seg_cnt, 0, ws)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
@@ -2104,27 +2372,37 @@ int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
     if (rc)
         return rc;
     hipStream_t s = c->stream;
+    const bool small = small_ok(c, n);
     GatherParams G;
     memset(&G, 0, sizeof(G));
-    // the pointer (and length) arrays are read in place when registered
+    // The pointer (and length) arrays are read in place when registered; else
+    // from the pinned staging, in place too on the small-burst path.
     G.ptrs = (const uint64_t *)dev_alias(c, ptrs, (size_t)n * 8);
     if (!G.ptrs) {
         memcpy(c->h_ptrs, ptrs, (size_t)n * 8);
-        YRSS_HIP(hipMemcpyAsync(c->d_ptrs, c->h_ptrs, (size_t)n * 8, hipMemcpyHostToDevice, s));
-        G.ptrs = c->d_ptrs;
+        if (small) {
+            G.ptrs = c->dh_ptrs;
+        } else {
+            YRSS_HIP(hipMemcpyAsync(c->d_ptrs, c->h_ptrs, (size_t)n * 8, hipMemcpyHostToDevice,
+                                    s));
+            G.ptrs = c->d_ptrs;
+        }
     }
     if (frames) {
         G.lens = (const uint16_t *)dev_alias(c, lens, (size_t)n * 2);
         if (!G.lens) {
             memcpy(c->h_len, lens, (size_t)n * 2);
-            YRSS_HIP(hipMemcpyAsync(c->d_q, c->h_len, (size_t)n * 2, hipMemcpyHostToDevice, s));
-            G.lens = (const uint16_t *)c->d_q;   // d_q is free until the parse kernel
+            if (small) {
+                G.lens = c->dh_len;
+            } else {
+                YRSS_HIP(hipMemcpyAsync(c->d_q, c->h_len, (size_t)n * 2, hipMemcpyHostToDevice,
+                                        s));
+                G.lens = (const uint16_t *)c->d_q;   // d_q is free until the parse kernel
+            }
         }
     }
-    YRSS_HIP(hipMemsetAsync(c->d_fault, 0, sizeof(uint32_t), s));
     G.win = c->d_win;
     G.len = c->d_len;
-    G.fault = c->d_fault;
     G.hash = c->d_hash;
     G.n = n;
     G.frames = frames ? 1u : 0u;
@@ -2134,11 +2412,56 @@ int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
     G.off_data_len = ml.off_data_len;
     G.off_hash_rss = ml.off_hash_rss;
     memcpy(G.ranges, c->ranges, sizeof(G.ranges));
+    const bool compact = out_qidx && out_qstart;
+    const bool want_hash = out_hash || (flags & YRSS_F_WRITE_RSS);
+    if (small) {
+        // one launch: gather + parse + lists, outputs straight to host memory
+        // (the caller's arrays when registered, else the pinned staging)
+        *c->h_fault = 0;
+        G.fault = c->dh_fault;
+        SmallParams S;
+        memset(&S, 0, sizeof(S));
+        S.G = G;
+        S.gather = 1;
+        S.writeback = (!frames && (flags & YRSS_F_WRITE_RSS)) ? 1u : 0u;
+        S.P.win = c->d_win;
+        S.P.len = c->d_len;
+        S.P.stride = YRSS_WIN_FULL;
+        S.P.n = n;
+        Out outs[4] = {{out_q, c->h_q, (size_t)n * 2, false},
+                       {out_hash, c->h_hash, (size_t)n * 4, false},
+                       {compact ? out_qidx : nullptr, c->h_qidx, (size_t)n * 4, false},
+                       {compact ? out_qstart : nullptr, c->h_qstart, (c->nb + 1) * 4, false}};
+        void *staged[4] = {c->dh_q, c->dh_hash, c->dh_qidx, c->dh_qstart};
+        void *dst[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (int k = 0; k < 4; ++k) {
+            if (!outs[k].user)
+                continue;
+            dst[k] = const_cast<void *>(dev_alias(c, outs[k].user, outs[k].bytes));
+            outs[k].direct = dst[k] != nullptr;
+            if (!dst[k])
+                dst[k] = staged[k];
+        }
+        S.P.q = (int16_t *)dst[0];
+        S.P.hash = (uint32_t *)dst[1];
+        S.qidx = (uint32_t *)dst[2];
+        S.qstart = (uint32_t *)dst[3];
+        (void)want_hash;   // the kernel keeps every hash in LDS for the write-back
+        if ((rc = small_launch(c, S, false)) != 0)
+            return rc;
+        YRSS_HIP(hipStreamSynchronize(s));
+        if (__atomic_load_n(c->h_fault, __ATOMIC_ACQUIRE))
+            return -EFAULT;
+        for (int k = 0; k < 4; ++k)
+            if (outs[k].user && !outs[k].direct)
+                memcpy(outs[k].user, outs[k].stage, outs[k].bytes);
+        return 0;
+    }
+    YRSS_HIP(hipMemsetAsync(c->d_fault, 0, sizeof(uint32_t), s));
+    G.fault = c->d_fault;
     const uint32_t blocks = std::min<uint32_t>((n + 63u) / 64u, (uint32_t)c->cus * 8u);
     hipLaunchKernelGGL(yrss_gather_zc, dim3(blocks), dim3(256), 0, s, G);
     YRSS_HIP(hipGetLastError());
-    const bool compact = out_qidx && out_qstart;
-    const bool want_hash = out_hash || (flags & YRSS_F_WRITE_RSS);
     yrss_dev_batch b;
     b.win = c->d_win;
     b.win_stride = YRSS_WIN_FULL;
