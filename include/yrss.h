@@ -193,9 +193,19 @@ int yrss_dispatch_dev_ex(yrss_ctx *ctx, const struct yrss_dev_batch *b, void *st
  *   out_hash   n x uint32 host array or NULL
  *   out_qidx / out_qstart  host arrays as in yrss_dispatch_dev, or NULL
  *   flags      YRSS_F_WRITE_RSS: also store each hash into mbuf hash.rss
- * Gathers min(data_len, 64 or 80) header bytes into pinned memory, copies to
- * the GPU, runs the same kernels, copies back.  Synchronous. */
+ * Gathers min(data_len, 64 or 80) header bytes into pinned memory.  Bursts of
+ * up to 4096 packets (with nb_queues + 1 <= 64) run as ONE kernel launch that
+ * reads the pinned windows and writes the pinned results in place; larger ones
+ * copy to the GPU, run the batch kernels and copy back.  Synchronous unless
+ * flags has YRSS_F_ASYNC. */
 #define YRSS_F_WRITE_RSS 0x1u
+/* Return once the burst is queued on the context's stream; the outputs (and the
+ * hash.rss write-back) are valid after yrss_wait(ctx) returns 0.  Everything
+ * the call reads in place (the mbufs, registered pointer/length arrays) and
+ * the output arrays must stay untouched until then.  One burst in flight per
+ * context: another host-resident call (or yrss_dispatch_dev*) returns -EBUSY
+ * until yrss_wait.  Pipeline bursts over several contexts (one per slot). */
+#define YRSS_F_ASYNC 0x2u
 int yrss_dispatch_burst(yrss_ctx *ctx, void *const *mbufs, uint32_t n,
                         int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx,
                         uint32_t *out_qstart, uint32_t flags);
@@ -207,7 +217,8 @@ int yrss_dispatch_burst(yrss_ctx *ctx, void *const *mbufs, uint32_t n,
  * straight from host memory, and with YRSS_F_WRITE_RSS writes hash.rss back
  * into the mbuf itself.  The dispatcher core does no per-packet work.
  * Returns -EFAULT if a mbuf or its data lies outside every registered range
- * (checked on the GPU; results are then not written). Synchronous. */
+ * (checked on the GPU; results are then not written).  Synchronous unless
+ * flags has YRSS_F_ASYNC. */
 int yrss_dispatch_burst_zc(yrss_ctx *ctx, void *const *mbufs, uint32_t n, int16_t *out_q,
                            uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
                            uint32_t flags);
@@ -222,6 +233,15 @@ int yrss_dispatch_burst_zc(yrss_ctx *ctx, void *const *mbufs, uint32_t n, int16_
 int yrss_dispatch_frames_zc(yrss_ctx *ctx, const uint8_t *const *data, const uint16_t *len,
                             uint32_t n, int16_t *out_q, uint32_t *out_hash,
                             uint32_t *out_qidx, uint32_t *out_qstart);
+/* Same, with flags (YRSS_F_ASYNC). */
+int yrss_dispatch_frames_zc_ex(yrss_ctx *ctx, const uint8_t *const *data, const uint16_t *len,
+                               uint32_t n, int16_t *out_q, uint32_t *out_hash,
+                               uint32_t *out_qidx, uint32_t *out_qstart, uint32_t flags);
+
+/* Complete the burst queued with YRSS_F_ASYNC: 0 (outputs valid), or the error
+ * the synchronous call would have returned (-EFAULT, -EIO, ...).  0 when
+ * nothing is in flight. */
+int yrss_wait(yrss_ctx *ctx);
 
 /* Register / unregister a host range (hipHostRegister, mapped) for the
  * zero-copy path; up to 16 ranges per context. */

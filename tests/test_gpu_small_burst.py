@@ -150,3 +150,73 @@ def test_small_and_multi_kernel_paths_agree(dev, oracle_mod, n, monkeypatch):
     q, h, qi, qs = _expect(oracle_mod, frames, (3, 3, 1, 1))
     _check(a, q, h, qi, qs)
     assert os.environ.get("YRSS_NO_SMALL") == "1"
+
+
+@pytest.mark.parametrize("n", [1000, 6000])   # one-launch path / multi-kernel path
+def test_async_bursts_over_two_contexts(dev, oracle_mod, n):
+    """YRSS_F_ASYNC: bursts in flight on two contexts sharing one registered
+    pool; -EBUSY for a second burst on a busy context; yrss_wait delivers."""
+    cfg = (5, 4, 1, 1)
+    frames = _frames(oracle_mod, 2 * n, 99)
+    q, h, qi, qs = _expect(oracle_mod, frames[:n], cfg)
+    q2, h2, qi2, qs2 = _expect(oracle_mod, frames[n:], cfg)
+    pool, ptrs, stride = _fake_mbufs(frames, headroom=128)
+    lib = abi.load()
+    outs = [(np.empty(n, np.int16), np.empty(n, np.uint32), np.empty(n, np.uint32),
+             np.empty(cfg[1] + 2, np.uint32)) for _ in range(2)]
+    with SoftRss(*cfg, device=0, max_burst=0) as e0, SoftRss(*cfg, device=0, max_burst=0) as e1:
+        for e in (e0, e1):
+            e.register_host_memory(pool.ctypes.data, pool.nbytes)   # refcounted
+        halves = [ptrs[:n].copy(), ptrs[n:].copy()]
+        for e, hp, o in zip((e0, e1), halves, outs):
+            rc = lib.yrss_dispatch_burst_zc(e._ctx, hp.ctypes.data, n, o[0].ctypes.data,
+                                            o[1].ctypes.data, o[2].ctypes.data,
+                                            o[3].ctypes.data, abi.F_ASYNC | abi.F_WRITE_RSS)
+            assert rc == 0
+        # a second burst on a busy context, and the device path, are refused
+        rc = lib.yrss_dispatch_burst_zc(e0._ctx, halves[0].ctypes.data, n, outs[0][0].ctypes.data,
+                                        None, None, None, 0)
+        assert rc == -16   # -EBUSY
+        assert lib.yrss_wait(e0._ctx) == 0
+        assert lib.yrss_wait(e1._ctx) == 0
+        assert lib.yrss_wait(e1._ctx) == 0   # nothing in flight
+        for o, (a, b, c_, d) in zip(outs, ((q, h, qi, qs), (q2, h2, qi2, qs2))):
+            assert np.array_equal(o[0], a) and np.array_equal(o[1], b)
+            assert np.array_equal(o[2], c_) and np.array_equal(o[3][: d.size], d)
+        rss = pool.reshape(-1, stride)[:, 44:48].copy().view(np.uint32).ravel()
+        assert np.array_equal(rss, np.concatenate([h, h2]))
+        # dropping one context's registration keeps the other's working
+        e0.unregister_host_memory(pool.ctypes.data)
+        _check(e1.dispatch_burst_zc(ptrs[:n]), q, h, qi, qs)
+        e1.unregister_host_memory(pool.ctypes.data)
+
+
+def test_async_staged_and_frames(dev, oracle_mod):
+    cfg = (8, 8, 1, 0)
+    n = 3000
+    frames = _frames(oracle_mod, n, 7)
+    q, h, qi, qs = _expect(oracle_mod, frames, cfg)
+    pool, ptrs, stride = _fake_mbufs(frames, headroom=130)
+    data = (ptrs + np.uint64(128 + 130)).astype(np.uint64)
+    flen = np.array([len(f) for f in frames], np.uint16)
+    lib = abi.load()
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        oq, oh = np.empty(n, np.int16), np.empty(n, np.uint32)
+        oqi, oqs = np.empty(n, np.uint32), np.empty(cfg[1] + 2, np.uint32)
+        rc = lib.yrss_dispatch_burst(eng._ctx, ptrs.ctypes.data, n, oq.ctypes.data,
+                                     None, oqi.ctypes.data, oqs.ctypes.data,
+                                     abi.F_ASYNC | abi.F_WRITE_RSS)
+        assert rc == 0
+        assert lib.yrss_wait(eng._ctx) == 0
+        assert np.array_equal(oq, q) and np.array_equal(oqi, qi)
+        assert np.array_equal(oqs[: qs.size], qs)
+        rss = pool.reshape(-1, stride)[:, 44:48].copy().view(np.uint32).ravel()
+        assert np.array_equal(rss, h)
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        rc = lib.yrss_dispatch_frames_zc_ex(eng._ctx, data.ctypes.data, flen.ctypes.data, n,
+                                            oq.ctypes.data, oh.ctypes.data, oqi.ctypes.data,
+                                            oqs.ctypes.data, abi.F_ASYNC)
+        assert rc == 0
+        assert lib.yrss_wait(eng._ctx) == 0
+        assert np.array_equal(oq, q) and np.array_equal(oh, h) and np.array_equal(oqi, qi)
+        eng.unregister_host_memory(pool.ctypes.data)

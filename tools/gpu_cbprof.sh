@@ -1,14 +1,10 @@
-# Host-resident burst latency: cbench at bursts 32 / 1024 (+ pool-size and THP
-# variants of the zero-copy mbuf path), then a kernel/API trace of burst_zc.
+# Host-resident burst rates (tools/yrss_cbench): bursts 32 / 1024 / 32K with 1, 2
+# and 4 bursts in flight (YRSS_F_ASYNC over that many contexts).
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-for b in 32 1024; do
-  YRSS_CBENCH_MODES=013 timeout -k 10 120 tools/yrss_cbench 1 65536 $b 1 > gpurun_out/cb$b.log 2>&1 || { cat gpurun_out/cb$b.log; exit 1; }
-  cat gpurun_out/cb$b.log | cut -c1-190
+for b in 32 1024 32768; do
+  for k in 1 2 4; do
+    YRSS_CBENCH_INFLIGHT=$k YRSS_CBENCH_MODES=013 timeout -k 10 120 tools/yrss_cbench 1 262144 $b 1 > gpurun_out/cb_${b}_$k.log 2>&1 || { cat gpurun_out/cb_${b}_$k.log; exit 1; }
+    python3 tools/cb_summary.py gpurun_out/cb_${b}_$k.log
+  done
 done
-for pool in 2048 1048576; do
-  YRSS_CBENCH_MODES=1 timeout -k 10 120 tools/yrss_cbench 1 $pool 1024 1 | cut -c1-170
-done
-YRSS_CBENCH_THP=0 YRSS_CBENCH_MODES=1 timeout -k 10 120 tools/yrss_cbench 1 65536 1024 1 | cut -c1-170
-YRSS_NO_SMALL=1 YRSS_CBENCH_MODES=013 timeout -k 10 120 tools/yrss_cbench 1 65536 1024 1 | cut -c1-170
-YRSS_CBENCH_MODES=1 timeout -k 10 200 rocprofv3 --kernel-trace --runtime-trace -d gpurun_out/cbprof -o run --output-format csv -- tools/yrss_cbench 1 65536 1024 1 > gpurun_out/cbprof.log 2>&1 || { tail gpurun_out/cbprof.log; exit 1; }

@@ -125,29 +125,45 @@ int main(int argc, char **argv)
         if (mode == 3)
             fill_frames(mbufs, pool, fdata, flen);    /* outside the timed region */
         cfg.max_burst = B;
-        yrss_ctx *ctx = NULL;
-        int rc = yrss_init(&cfg, &ctx);
-        if (rc) {
-            fprintf(stderr, "yrss_init: %d\n", rc);
-            return 2;
+        /* YRSS_CBENCH_INFLIGHT=k: k contexts, bursts submitted with YRSS_F_ASYNC
+         * round-robin, each context waited on before its next submit */
+        const char *inf_env = getenv("YRSS_CBENCH_INFLIGHT");
+        unsigned K = inf_env ? (unsigned)atoi(inf_env) : 1u;
+        if (K < 1)
+            K = 1;
+        if (K > 8)
+            K = 8;
+        if ((uint64_t)K * B > pool)
+            K = pool / B ? pool / B : 1;
+        const uint32_t aflag = K > 1 ? YRSS_F_ASYNC : 0u;
+        yrss_ctx *ctxs[8] = {0};
+        int rc = 0;
+        for (unsigned k = 0; k < K; ++k) {
+            if ((rc = yrss_init(&cfg, &ctxs[k])) != 0) {
+                fprintf(stderr, "yrss_init: %d\n", rc);
+                return 2;
+            }
+            if (mode >= 1 && ((rc = yrss_register_host_memory(ctxs[k], mem, mem_sz)) ||
+                              (rc = yrss_register_host_memory(ctxs[k], arena, arena_sz)))) {
+                fprintf(stderr, "yrss_register_host_memory: %d\n", rc);
+                return 2;
+            }
         }
-        if (mode >= 1 && ((rc = yrss_register_host_memory(ctx, mem, mem_sz)) ||
-                          (rc = yrss_register_host_memory(ctx, arena, arena_sz)))) {
-            fprintf(stderr, "yrss_register_host_memory: %d\n", rc);
-            return 2;
-        }
-        int16_t *q = q_all;
-        uint32_t *h = h_all, *qi = qi_all;
-        uint32_t qs[YRSS_MAX_QUEUES + 2];
-        /* one burst: what the dispatcher lcore would do after rte_eth_rx_burst */
-        #define RUN_BURST(off) ( \
-            mode == 0 ? yrss_dispatch_burst(ctx, mbufs + (off), B, q, h, qi, qs, 0) : \
-            mode == 1 ? yrss_dispatch_burst_zc(ctx, mbufs + (off), B, q, h, qi, qs, 0) : \
+        yrss_ctx *ctx = ctxs[0];
+        static uint32_t qs[8][YRSS_MAX_QUEUES + 2];
+        /* one burst: what the dispatcher lcore would do after rte_eth_rx_burst;
+         * outputs land in the burst's own slice of the (registered) arena */
+        #define RUN_BURST(cx, k, off) ( \
+            mode == 0 ? yrss_dispatch_burst(cx, mbufs + (off), B, q_all + (off), h_all + (off), \
+                                            qi_all + (off), qs[k], aflag) : \
+            mode == 1 ? yrss_dispatch_burst_zc(cx, mbufs + (off), B, q_all + (off), \
+                                               h_all + (off), qi_all + (off), qs[k], aflag) : \
             ((mode == 2 ? fill_frames(mbufs + (off), B, fdata + (off), flen + (off)) : (void)0), \
-             yrss_dispatch_frames_zc(ctx, fdata + (off), flen + (off), B, q, h, qi, qs)))
+             yrss_dispatch_frames_zc_ex(cx, fdata + (off), flen + (off), B, q_all + (off), \
+                                        h_all + (off), qi_all + (off), qs[k], aflag)))
         /* warm up */
         for (uint32_t off = 0; off + B <= pool && off < 4 * B; off += B)
-            if ((rc = RUN_BURST(off)) != 0) {
+            if ((rc = RUN_BURST(ctx, 0, off)) != 0 || (rc = yrss_wait(ctx)) != 0) {
                 fprintf(stderr, "dispatch: %d\n", rc);
                 return 3;
             }
@@ -155,26 +171,43 @@ int main(int argc, char **argv)
         const double t0 = now();
         double t1 = t0;
         uint32_t off = 0;
+        uint64_t i = 0;
+        int busy[8] = {0};
         while (t1 - t0 < secs) {
             if (off + B > pool)
                 off = 0;
-            rc = RUN_BURST(off);
+            const unsigned k = (unsigned)(i % K);
+            if (busy[k] && (rc = yrss_wait(ctxs[k])) != 0) {
+                fprintf(stderr, "wait: %d\n", rc);
+                return 3;
+            }
+            rc = RUN_BURST(ctxs[k], k, off);
             if (rc) {
                 fprintf(stderr, "dispatch: %d\n", rc);
                 return 3;
             }
+            busy[k] = K > 1;
             off += B;
             pkts += B;
+            ++i;
             t1 = now();
         }
+        for (unsigned k = 0; k < K; ++k)
+            if (busy[k] && (rc = yrss_wait(ctxs[k])) != 0) {
+                fprintf(stderr, "wait: %d\n", rc);
+                return 3;
+            }
+        t1 = now();
         printf("{\"tool\": \"yrss_cbench\", \"api\": \"%s\", \"profile\": %u, "
-               "\"burst\": %u, \"pkts\": %llu, \"seconds\": %.3f, \"mpps\": %.2f, "
-               "\"us_per_burst\": %.2f, \"queue_of_first\": %d, \"thp\": %d, "
+               "\"burst\": %u, \"inflight\": %u, \"pkts\": %llu, \"seconds\": %.3f, "
+               "\"mpps\": %.2f, \"us_per_burst\": %.2f, \"queue_of_first\": %d, \"thp\": %d, "
                "\"mode\": %u, \"note\": \"%s\"}\n",
-               names[mode], profile, B,
+               names[mode], profile, B, K,
                (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
-               (t1 - t0) / (pkts / (double)B) * 1e6, q[0], thp, mode, notes[mode]);
+               (t1 - t0) / (pkts / (double)B) * 1e6, q_all[0], thp, mode, notes[mode]);
         fflush(stdout);
+        for (unsigned k = 1; k < K; ++k)
+            yrss_fini(ctxs[k]);
         yrss_fini(ctx);                 /* also unregisters the pool */
         if (burst_arg)
             break;

@@ -27,6 +27,7 @@ WIN_FULL = 80
 MAX_QUEUES = 256
 MAX_PROCS = 4096
 F_WRITE_RSS = 0x1
+F_ASYNC = 0x2
 
 K_PARSE_HASH, K_SCAN, K_SCATTER = 0, 1, 2
 
@@ -147,6 +148,9 @@ _PROTOS = {
                                         ctypes.POINTER(_u32)]),
     "yrss_grid_for": (_u32, [_vp, _u32]),
     "yrss_status": (ctypes.c_int, [_vp]),
+    "yrss_wait": (ctypes.c_int, [_vp]),
+    "yrss_dispatch_frames_zc_ex": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp,
+                                                  _u32]),
     "yrss_set_kni": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
                                     ctypes.c_char_p]),
     "yrss_dispatch_dev_ex": (ctypes.c_int, [_vp, ctypes.POINTER(DevBatch), _vp]),

@@ -36,6 +36,8 @@
 #include <algorithm>
 #include <strings.h>
 
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "yrss.h"
@@ -1423,6 +1425,27 @@ struct TimedPair {
     int kernel;
 };
 
+// A host output array: written in place when it is registered (the kernel or
+// the DMA writes it directly), else through the context's pinned staging and
+// copied when the burst completes.
+struct HostOut {
+    void *user;
+    void *stage;
+    size_t bytes;
+    bool direct;
+};
+
+// The host-resident burst in flight on the context stream.  Synchronous calls
+// complete it before returning; YRSS_F_ASYNC leaves it for yrss_wait.
+struct PendingBurst {
+    bool active = false;
+    uint32_t n = 0;
+    HostOut outs[5] = {};            // q, hash, qidx, qstart, filter
+    bool gather_fault = false;       // zero-copy: a pointer outside every range
+    bool scan_fault = false;         // multi-kernel path: scan look-back fault
+    void *const *wb_mbufs = nullptr; // host-side hash.rss write-back (staged path)
+};
+
 struct yrss_ctx {
     yrss_config cfg;
     int device = 0;
@@ -1492,6 +1515,7 @@ struct yrss_ctx {
     int8_t *dh_filter = nullptr;
     uint64_t *dh_ptrs = nullptr;
     uint32_t *dh_fault = nullptr;
+    PendingBurst pend;
     // timing
     uint32_t timing_mask = 0;    // bit k: bracket kernel k with events
     std::vector<hipEvent_t> ev_free;
@@ -1744,6 +1768,44 @@ int ensure_burst(yrss_ctx *c, uint32_t n)
 // Host-staged classification shared by the burst/frames/route entry points.
 // The windows and data_len are already gathered into c->h_win / c->h_len at
 // stride W; results land in the caller's host arrays (NULL = not wanted).
+// hipHostRegister is process-wide, but each context keeps its own range table
+// (several contexts pipeline bursts over one mbuf pool), so registrations are
+// reference-counted per (base, len).
+struct HostReg {
+    size_t len;
+    uint32_t refs;
+};
+std::mutex g_reg_mu;
+std::map<void *, HostReg> g_reg;
+
+hipError_t host_reg_acquire(void *base, size_t len)
+{
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.find(base);
+    if (it != g_reg.end()) {
+        if (it->second.len != len)
+            return hipErrorHostMemoryAlreadyRegistered;
+        ++it->second.refs;
+        return hipSuccess;
+    }
+    const hipError_t e = hipHostRegister(base, len, hipHostRegisterMapped);
+    if (e == hipSuccess)
+        g_reg[base] = HostReg{len, 1u};
+    return e;
+}
+
+void host_reg_release(void *base)
+{
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.find(base);
+    if (it == g_reg.end())
+        return;
+    if (--it->second.refs == 0) {
+        (void)hipHostUnregister(base);
+        g_reg.erase(it);
+    }
+}
+
 // A scan look-back that never resolved leaves that batch's lists invalid.
 bool take_scan_fault(yrss_ctx *c)
 {
@@ -1752,6 +1814,8 @@ bool take_scan_fault(yrss_ctx *c)
         fprintf(stderr, "yrss: scan look-back did not resolve; per-queue lists invalid\n");
     return f != 0;
 }
+
+int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream);
 
 bool small_ok(const yrss_ctx *c, uint32_t n)
 {
@@ -1784,11 +1848,48 @@ int small_launch(yrss_ctx *c, SmallParams &S, bool filter)
     return 0;
 }
 
+// Completes the pending host burst: waits for the stream, checks the device
+// fault words, copies staged outputs and writes hash.rss back on the host.
+int finish_burst(yrss_ctx *c)
+{
+    PendingBurst &p = c->pend;
+    if (!p.active)
+        return 0;
+    p.active = false;
+    YRSS_HIP(hipStreamSynchronize(c->stream));
+    if (p.gather_fault && __atomic_load_n(c->h_fault, __ATOMIC_ACQUIRE))
+        return -EFAULT;
+    if (p.scan_fault && take_scan_fault(c))
+        return -EIO;
+    for (int k = 0; k < 5; ++k)
+        if (p.outs[k].user && !p.outs[k].direct)
+            memcpy(p.outs[k].user, p.outs[k].stage, p.outs[k].bytes);
+    if (p.wb_mbufs) {
+        const uint8_t *h = (const uint8_t *)(p.outs[1].user ? p.outs[1].user : p.outs[1].stage);
+        for (uint32_t i = 0; i < p.n; ++i)
+            memcpy((uint8_t *)p.wb_mbufs[i] + c->cfg.mbuf.off_hash_rss, h + 4u * i, 4);
+    }
+    return 0;
+}
+
+// Queues the classification of windows already gathered into c->h_win /
+// c->h_len at stride W; results go to the caller's host arrays (NULL = not
+// wanted) when the burst completes (finish_burst).  want_hash computes the
+// hash into the staging even without out_hash (hash.rss write-back).
 int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_t *out_hash,
-                    uint32_t *out_qidx, uint32_t *out_qstart, int8_t *out_filter)
+                    uint32_t *out_qidx, uint32_t *out_qstart, int8_t *out_filter, bool want_hash)
 {
     hipStream_t s = c->stream;
     const bool compact = out_qidx && out_qstart;
+    want_hash = want_hash || out_hash;
+    PendingBurst &p = c->pend;
+    p = PendingBurst{};
+    p.n = n;
+    p.outs[0] = {out_q, c->h_q, (size_t)n * 2, false};
+    p.outs[1] = {out_hash, c->h_hash, (size_t)n * 4, false};
+    p.outs[2] = {compact ? out_qidx : nullptr, c->h_qidx, (size_t)n * 4, false};
+    p.outs[3] = {compact ? out_qstart : nullptr, c->h_qstart, (c->nb + 1) * 4, false};
+    p.outs[4] = {out_filter, c->h_filter, n, false};
     if (small_ok(c, n)) {
         // the kernel reads the staged windows and writes the staging in place
         SmallParams S;
@@ -1798,23 +1899,14 @@ int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_
         S.P.stride = W;
         S.P.n = n;
         S.P.q = c->dh_q;
-        S.P.hash = out_hash ? c->dh_hash : nullptr;
+        S.P.hash = want_hash ? c->dh_hash : nullptr;
         S.P.filter = out_filter ? c->dh_filter : nullptr;
         S.qidx = compact ? c->dh_qidx : nullptr;
         S.qstart = compact ? c->dh_qstart : nullptr;
         int rc = small_launch(c, S, out_filter != nullptr);
         if (rc)
             return rc;
-        YRSS_HIP(hipStreamSynchronize(s));
-        memcpy(out_q, c->h_q, (size_t)n * 2);
-        if (out_hash)
-            memcpy(out_hash, c->h_hash, (size_t)n * 4);
-        if (out_filter)
-            memcpy(out_filter, c->h_filter, n);
-        if (compact) {
-            memcpy(out_qidx, c->h_qidx, (size_t)n * 4);
-            memcpy(out_qstart, c->h_qstart, (c->nb + 1) * 4);
-        }
+        p.active = true;
         return 0;
     }
     YRSS_HIP(hipMemcpyAsync(c->d_win, c->h_win, (size_t)n * W, hipMemcpyHostToDevice, s));
@@ -1825,15 +1917,15 @@ int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_
     b.n = n;
     b.len = c->d_len;
     b.q = c->d_q;
-    b.hash = out_hash ? c->d_hash : nullptr;
+    b.hash = want_hash ? c->d_hash : nullptr;
     b.qidx = compact ? c->d_qidx : nullptr;
     b.qstart = compact ? c->d_qstart : nullptr;
     b.filter = out_filter ? c->d_filter : nullptr;
-    int rc = yrss_dispatch_dev_ex(c, &b, s);
+    int rc = dispatch_dev_impl(c, &b, s);
     if (rc)
         return rc;
     YRSS_HIP(hipMemcpyAsync(c->h_q, c->d_q, (size_t)n * 2, hipMemcpyDeviceToHost, s));
-    if (out_hash)
+    if (want_hash)
         YRSS_HIP(hipMemcpyAsync(c->h_hash, c->d_hash, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     if (out_filter)
         YRSS_HIP(hipMemcpyAsync(c->h_filter, c->d_filter, n, hipMemcpyDeviceToHost, s));
@@ -1842,19 +1934,18 @@ int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_
         YRSS_HIP(hipMemcpyAsync(c->h_qstart, c->d_qstart, (c->nb + 1) * 4,
                                 hipMemcpyDeviceToHost, s));
     }
-    YRSS_HIP(hipStreamSynchronize(s));
-    if (compact && take_scan_fault(c))
-        return -EIO;
-    memcpy(out_q, c->h_q, (size_t)n * 2);
-    if (out_hash)
-        memcpy(out_hash, c->h_hash, (size_t)n * 4);
-    if (out_filter)
-        memcpy(out_filter, c->h_filter, n);
-    if (compact) {
-        memcpy(out_qidx, c->h_qidx, (size_t)n * 4);
-        memcpy(out_qstart, c->h_qstart, (c->nb + 1) * 4);
-    }
+    p.scan_fault = compact;
+    p.active = true;
     return 0;
+}
+
+// Host entry points: one burst in flight per context.  begin_burst refuses a
+// second one; end_burst completes it unless the caller asked for YRSS_F_ASYNC.
+int begin_burst(const yrss_ctx *c) { return c->pend.active ? -EBUSY : 0; }
+
+int end_burst(yrss_ctx *c, uint32_t flags)
+{
+    return (flags & YRSS_F_ASYNC) ? 0 : finish_burst(c);
 }
 
 // Window stride for a host batch: 64 bytes when every frame fits, else 80
@@ -2044,6 +2135,7 @@ void yrss_fini(yrss_ctx *c)
     if (!c)
         return;
     (void)hipSetDevice(c->device);
+    c->pend.active = false;   // its outputs are abandoned with the context
     if (c->stream)
         (void)hipStreamSynchronize(c->stream);
     for (auto &p : c->ev_pending) {
@@ -2063,7 +2155,7 @@ void yrss_fini(yrss_ctx *c)
     (void)hipFree(c->d_fault);
     (void)hipHostFree(c->h_fault);
     for (uint32_t r = 0; r < c->nranges; ++r)
-        (void)hipHostUnregister(c->range_base[r]);
+        host_reg_release(c->range_base[r]);
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
     delete c;
@@ -2100,6 +2192,17 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
 {
     if (!c || !b)
         return -EINVAL;
+    if (c->pend.active)      // the host burst in flight owns the workspace
+        return -EBUSY;
+    return dispatch_dev_impl(c, b, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
+{
     const uint32_t n = b->n, win_stride = b->win_stride;
     if (win_stride < YRSS_WIN_MIN || (win_stride & 15u) || n > YRSS_MAX_BATCH)
         return -EINVAL;
@@ -2218,6 +2321,10 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     return 0;
 }
 
+}  // namespace
+
+extern "C" {
+
 int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
                       const uint16_t *d_len, uint32_t n, int16_t *d_q, uint32_t *d_hash,
                       uint32_t *d_qidx, uint32_t *d_qstart, void *stream)
@@ -2246,9 +2353,11 @@ int yrss_dispatch_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t
             memset(out_qstart, 0, (c->nb + 1) * sizeof(uint32_t));
         return 0;
     }
-    YRSS_HIP(hipSetDevice(c->device));
-    int rc = ensure_burst(c, n);
+    int rc = begin_burst(c);
     if (rc)
+        return rc;
+    YRSS_HIP(hipSetDevice(c->device));
+    if ((rc = ensure_burst(c, n)) != 0)
         return rc;
     uint32_t maxlen = 0;
     for (uint32_t i = 0; i < n; ++i)
@@ -2259,7 +2368,10 @@ int yrss_dispatch_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t
         memcpy(c->h_win + (size_t)i * W, data[i], L < W ? L : W);
         c->h_len[i] = (uint16_t)L;
     }
-    return classify_staged(c, n, W, out_q, out_hash, out_qidx, out_qstart, nullptr);
+    if ((rc = classify_staged(c, n, W, out_q, out_hash, out_qidx, out_qstart, nullptr,
+                              false)) != 0)
+        return rc;
+    return finish_burst(c);
 }
 
 int yrss_dispatch_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out_q,
@@ -2273,24 +2385,19 @@ int yrss_dispatch_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *ou
             memset(out_qstart, 0, (c->nb + 1) * sizeof(uint32_t));
         return 0;
     }
+    int rc = begin_burst(c);
+    if (rc)
+        return rc;
     YRSS_HIP(hipSetDevice(c->device));
     uint32_t W = 0;
-    int rc = gather_mbufs(c, mbufs, n, &W);
-    if (rc)
+    if ((rc = gather_mbufs(c, mbufs, n, &W)) != 0)
         return rc;
-    uint32_t *hash = out_hash;
-    std::vector<uint32_t> tmp;
-    if (!hash && (flags & YRSS_F_WRITE_RSS)) {
-        tmp.resize(n);
-        hash = tmp.data();
-    }
-    rc = classify_staged(c, n, W, out_q, hash, out_qidx, out_qstart, nullptr);
-    if (rc)
+    const bool wb = (flags & YRSS_F_WRITE_RSS) != 0;
+    if ((rc = classify_staged(c, n, W, out_q, out_hash, out_qidx, out_qstart, nullptr, wb)) != 0)
         return rc;
-    if (flags & YRSS_F_WRITE_RSS)
-        for (uint32_t i = 0; i < n; ++i)
-            memcpy((uint8_t *)mbufs[i] + c->cfg.mbuf.off_hash_rss, &hash[i], 4);
-    return 0;
+    if (wb)
+        c->pend.wb_mbufs = mbufs;
+    return end_burst(c, flags);
 }
 
 int yrss_register_host_memory(yrss_ctx *c, void *base, size_t len)
@@ -2298,11 +2405,11 @@ int yrss_register_host_memory(yrss_ctx *c, void *base, size_t len)
     if (!c || !base || !len || c->nranges >= YRSS_MAX_HOST_RANGES)
         return -EINVAL;
     YRSS_HIP(hipSetDevice(c->device));
-    YRSS_HIP(hipHostRegister(base, len, hipHostRegisterMapped));
+    YRSS_HIP(host_reg_acquire(base, len));
     void *dev = nullptr;
     hipError_t e = hipHostGetDevicePointer(&dev, base, 0);
     if (e != hipSuccess) {
-        (void)hipHostUnregister(base);
+        host_reg_release(base);
         return hip_fail("hipHostGetDevicePointer", e);
     }
     HostRange &r = c->ranges[c->nranges];
@@ -2320,7 +2427,7 @@ int yrss_unregister_host_memory(yrss_ctx *c, void *base)
     for (uint32_t r = 0; r < c->nranges; ++r)
         if (c->range_base[r] == base) {
             YRSS_HIP(hipSetDevice(c->device));
-            YRSS_HIP(hipHostUnregister(base));
+            host_reg_release(base);
             for (uint32_t k = r + 1; k < c->nranges; ++k) {
                 c->ranges[k - 1] = c->ranges[k];
                 c->range_base[k - 1] = c->range_base[k];
@@ -2344,15 +2451,6 @@ const void *dev_alias(const yrss_ctx *c, const void *p, size_t bytes)
     return nullptr;
 }
 
-// D2H into a caller array: straight DMA when the array is registered (pinned),
-// else through the pinned staging (then copied after the sync).
-struct Out {
-    void *user;
-    void *stage;
-    size_t bytes;
-    bool direct;
-};
-
 int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n, bool frames,
                 int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
                 uint32_t flags)
@@ -2367,9 +2465,11 @@ int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
             memset(out_qstart, 0, (c->nb + 1) * sizeof(uint32_t));
         return 0;
     }
-    YRSS_HIP(hipSetDevice(c->device));
-    int rc = ensure_burst(c, n);
+    int rc = begin_burst(c);
     if (rc)
+        return rc;
+    YRSS_HIP(hipSetDevice(c->device));
+    if ((rc = ensure_burst(c, n)) != 0)
         return rc;
     hipStream_t s = c->stream;
     const bool small = small_ok(c, n);
@@ -2414,6 +2514,16 @@ int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
     memcpy(G.ranges, c->ranges, sizeof(G.ranges));
     const bool compact = out_qidx && out_qstart;
     const bool want_hash = out_hash || (flags & YRSS_F_WRITE_RSS);
+    PendingBurst &p = c->pend;
+    p = PendingBurst{};
+    p.n = n;
+    p.outs[0] = {out_q, c->h_q, (size_t)n * 2, false};
+    p.outs[1] = {out_hash, c->h_hash, (size_t)n * 4, false};
+    p.outs[2] = {compact ? out_qidx : nullptr, c->h_qidx, (size_t)n * 4, false};
+    p.outs[3] = {compact ? out_qstart : nullptr, c->h_qstart, (c->nb + 1) * 4, false};
+    p.gather_fault = true;
+    for (int k = 0; k < 4; ++k)
+        p.outs[k].direct = p.outs[k].user && dev_alias(c, p.outs[k].user, p.outs[k].bytes);
     if (small) {
         // one launch: gather + parse + lists, outputs straight to host memory
         // (the caller's arrays when registered, else the pinned staging)
@@ -2428,33 +2538,20 @@ int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
         S.P.len = c->d_len;
         S.P.stride = YRSS_WIN_FULL;
         S.P.n = n;
-        Out outs[4] = {{out_q, c->h_q, (size_t)n * 2, false},
-                       {out_hash, c->h_hash, (size_t)n * 4, false},
-                       {compact ? out_qidx : nullptr, c->h_qidx, (size_t)n * 4, false},
-                       {compact ? out_qstart : nullptr, c->h_qstart, (c->nb + 1) * 4, false}};
         void *staged[4] = {c->dh_q, c->dh_hash, c->dh_qidx, c->dh_qstart};
         void *dst[4] = {nullptr, nullptr, nullptr, nullptr};
-        for (int k = 0; k < 4; ++k) {
-            if (!outs[k].user)
-                continue;
-            dst[k] = const_cast<void *>(dev_alias(c, outs[k].user, outs[k].bytes));
-            outs[k].direct = dst[k] != nullptr;
-            if (!dst[k])
-                dst[k] = staged[k];
-        }
+        for (int k = 0; k < 4; ++k)
+            if (p.outs[k].user)
+                dst[k] = p.outs[k].direct
+                             ? const_cast<void *>(dev_alias(c, p.outs[k].user, p.outs[k].bytes))
+                             : staged[k];
         S.P.q = (int16_t *)dst[0];
-        S.P.hash = (uint32_t *)dst[1];
+        S.P.hash = (uint32_t *)dst[1];   // the kernel keeps every hash for the write-back
         S.qidx = (uint32_t *)dst[2];
         S.qstart = (uint32_t *)dst[3];
-        (void)want_hash;   // the kernel keeps every hash in LDS for the write-back
         if ((rc = small_launch(c, S, false)) != 0)
             return rc;
-        YRSS_HIP(hipStreamSynchronize(s));
-        if (__atomic_load_n(c->h_fault, __ATOMIC_ACQUIRE))
-            return -EFAULT;
-        for (int k = 0; k < 4; ++k)
-            if (outs[k].user && !outs[k].direct)
-                memcpy(outs[k].user, outs[k].stage, outs[k].bytes);
+        p.active = true;
         return 0;
     }
     YRSS_HIP(hipMemsetAsync(c->d_fault, 0, sizeof(uint32_t), s));
@@ -2472,33 +2569,22 @@ int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
     b.qidx = compact ? c->d_qidx : nullptr;
     b.qstart = compact ? c->d_qstart : nullptr;
     b.filter = nullptr;
-    if ((rc = yrss_dispatch_dev_ex(c, &b, s)) != 0)
+    if ((rc = dispatch_dev_impl(c, &b, s)) != 0)
         return rc;
     if (!frames && (flags & YRSS_F_WRITE_RSS)) {
         hipLaunchKernelGGL(yrss_writeback_zc, dim3((n + 255u) / 256u), dim3(256), 0, s, G);
         YRSS_HIP(hipGetLastError());
     }
-    Out outs[4] = {{out_q, c->h_q, (size_t)n * 2, false},
-                   {out_hash, c->h_hash, (size_t)n * 4, false},
-                   {compact ? out_qidx : nullptr, c->h_qidx, (size_t)n * 4, false},
-                   {compact ? out_qstart : nullptr, c->h_qstart, (c->nb + 1) * 4, false}};
     const void *src[4] = {c->d_q, c->d_hash, c->d_qidx, c->d_qstart};
     YRSS_HIP(hipMemcpyAsync(c->h_fault, c->d_fault, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     for (int k = 0; k < 4; ++k) {
-        if (!outs[k].user)
+        if (!p.outs[k].user)
             continue;
-        outs[k].direct = dev_alias(c, outs[k].user, outs[k].bytes) != nullptr;
-        YRSS_HIP(hipMemcpyAsync(outs[k].direct ? outs[k].user : outs[k].stage, src[k],
-                                outs[k].bytes, hipMemcpyDeviceToHost, s));
+        YRSS_HIP(hipMemcpyAsync(p.outs[k].direct ? p.outs[k].user : p.outs[k].stage, src[k],
+                                p.outs[k].bytes, hipMemcpyDeviceToHost, s));
     }
-    YRSS_HIP(hipStreamSynchronize(s));
-    if (*c->h_fault)
-        return -EFAULT;
-    if (compact && take_scan_fault(c))
-        return -EIO;
-    for (int k = 0; k < 4; ++k)
-        if (outs[k].user && !outs[k].direct)
-            memcpy(outs[k].user, outs[k].stage, outs[k].bytes);
+    p.scan_fault = compact;
+    p.active = true;
     return 0;
 }
 
@@ -2510,17 +2596,35 @@ int yrss_dispatch_burst_zc(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t 
 {
     if (!c || (n && (!mbufs || !out_q)))
         return -EINVAL;
-    return zc_dispatch(c, mbufs, nullptr, n, false, out_q, out_hash, out_qidx, out_qstart,
-                       flags);
+    const int rc = zc_dispatch(c, mbufs, nullptr, n, false, out_q, out_hash, out_qidx,
+                               out_qstart, flags);
+    return rc ? rc : end_burst(c, flags);
+}
+
+int yrss_dispatch_frames_zc_ex(yrss_ctx *c, const uint8_t *const *data, const uint16_t *len,
+                               uint32_t n, int16_t *out_q, uint32_t *out_hash,
+                               uint32_t *out_qidx, uint32_t *out_qstart, uint32_t flags)
+{
+    if (!c || (n && (!data || !len || !out_q)) || (flags & ~YRSS_F_ASYNC))
+        return -EINVAL;
+    const int rc = zc_dispatch(c, data, len, n, true, out_q, out_hash, out_qidx, out_qstart,
+                               flags);
+    return rc ? rc : end_burst(c, flags);
 }
 
 int yrss_dispatch_frames_zc(yrss_ctx *c, const uint8_t *const *data, const uint16_t *len,
                             uint32_t n, int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx,
                             uint32_t *out_qstart)
 {
-    if (!c || (n && (!data || !len || !out_q)))
+    return yrss_dispatch_frames_zc_ex(c, data, len, n, out_q, out_hash, out_qidx, out_qstart, 0);
+}
+
+int yrss_wait(yrss_ctx *c)
+{
+    if (!c)
         return -EINVAL;
-    return zc_dispatch(c, data, len, n, true, out_q, out_hash, out_qidx, out_qstart, 0);
+    YRSS_HIP(hipSetDevice(c->device));
+    return finish_burst(c);
 }
 
 int yrss_route_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, uint16_t queue_id,
@@ -2533,15 +2637,20 @@ int yrss_route_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, uint16_t queue
     memset(res, 0, sizeof(*res));
     if (n == 0)
         return 0;
+    int rc = begin_burst(c);
+    if (rc)
+        return rc;
     YRSS_HIP(hipSetDevice(c->device));
     uint32_t W = 0;
-    int rc = gather_mbufs(c, mbufs, n, &W);
-    if (rc)
+    if ((rc = gather_mbufs(c, mbufs, n, &W)) != 0)
         return rc;
     std::vector<int16_t> q(n);
     std::vector<int8_t> fc(n);
     std::vector<uint32_t> qidx(n), qstart(c->nb + 1);
-    rc = classify_staged(c, n, W, q.data(), nullptr, qidx.data(), qstart.data(), fc.data());
+    rc = classify_staged(c, n, W, q.data(), nullptr, qidx.data(), qstart.data(), fc.data(),
+                         false);
+    if (rc == 0)
+        rc = finish_burst(c);
     if (rc)
         return rc;
     const uint32_t nq = c->cfg.nb_queues;
