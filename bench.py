@@ -201,18 +201,21 @@ def probe_traffic(win, lens, out, n, stride, steps):
 
 def pcie_inclusive(profile: str):
     """Host-resident rates from tools/yrss_cbench (C host over the C ABI):
-    DPDK-layout mbuf pool of 2^20 packets in host memory, bursts of 32K and 1M."""
+    DPDK-layout mbuf pool of 2^20 packets in host memory; bursts of 1024 (BASELINE's
+    logical burst) and 32K with two in flight, and 1M."""
     import subprocess
 
     exe = ROOT / "tools" / "yrss_cbench"
     if not exe.exists():
         return None
     out = []
-    for burst in (32768, 1 << 20):
+    # (burst, bursts in flight over that many contexts with YRSS_F_ASYNC)
+    for burst, inflight in ((1024, 2), (32768, 2), (1 << 20, 1)):
         try:
             r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
-                               env={**os.environ, "YRSS_CBENCH_MODES": "013"})
+                               env={**os.environ, "YRSS_CBENCH_MODES": "013",
+                                    "YRSS_CBENCH_INFLIGHT": str(inflight)})
         except subprocess.TimeoutExpired:
             return None
         for line in r.stdout.splitlines():
@@ -220,8 +223,8 @@ def pcie_inclusive(profile: str):
                 d = json.loads(line)
             except ValueError:
                 continue
-            out.append({"api": d["api"], "burst": d["burst"], "mpps": d["mpps"],
-                        "note": d.get("note", "")})
+            out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
+                        "mpps": d["mpps"], "note": d.get("note", "")})
     return out or None
 
 

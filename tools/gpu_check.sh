@@ -32,13 +32,14 @@ if want bench; then
     step bench 600 python bench.py || exit 1
 fi
 if want prof; then
+    # the bench command itself under the profiler: the JSON line it prints
+    # (prof.log) and the kernel stats come from one process
     step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-        --output-format csv -- python bench.py --steps 20 --warmup 5 --cpu-seconds 0 --check 0 \
-        || exit 1
+        --output-format csv -- python bench.py || exit 1
     find gpurun_out/prof -name '*stats*' | head
 fi
 if want pmc; then
-    BENCH="python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --check 0"
+    BENCH="python bench.py --steps 10 --warmup 3 --cpu-seconds 0 --check 0 --pcie 0"
     step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run \
         --output-format csv -- $BENCH || exit 1
     step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run \
@@ -49,5 +50,6 @@ if want pmc; then
 fi
 if want cbench; then
     step cbench 600 tools/yrss_cbench 1 1048576 0 2 || exit 1
+    step host_async 600 bash tools/gpu_cbprof.sh || exit 1
 fi
 echo "== done"
