@@ -86,7 +86,7 @@ struct ParseParams {
     int8_t *filter;       // protocol_filter class per packet, or null
     const uint32_t *kni_bm;   // tcp bitmap (2048 words) then udp bitmap (2048 words)
     uint32_t kni_enable;
-    uint32_t pad_;
+    uint32_t out16;       // q/hash bursts as 16-byte stores: 1 plain, 2 sc1 (YRSS_OUT16)
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
@@ -240,12 +240,15 @@ struct OutSlot {
     uint16_t *r;
 };
 
-// Writes kOutTiles (or fewer) buffered tiles starting at packet t_first: plain
-// lane-granular stores issued back to back.  Bursts at batch end ran 4-5 %
-// faster than per-tile stores interleaved with the read stream (kernel 200 vs
-// 209 us on one box; tools/hbm_bw.hip "chunk4B-dflt" vs "tile-nt"), and the
-// default policy beat non-temporal (which also evicted q before the scatter
-// re-reads it: scatter 21.6 vs 25.5 us).
+// Writes kOutTiles (or fewer) buffered tiles starting at packet t_first,
+// issued back to back.  Bursts at batch end ran 4-5 % faster than per-tile
+// stores interleaved with the read stream (kernel 200 vs 209 us on one box;
+// tools/hbm_bw.hip "chunk4B-dflt" vs "tile-nt"), and the default policy beat
+// non-temporal (which also evicted q before the scatter re-reads it: scatter
+// 21.6 vs 25.5 us).  A full batch goes out as 16-byte write-through (sc1)
+// stores, 0.8 % faster than lane-granular plain stores and 1.8 % faster than
+// 16-byte plain ones (profiles/r01_v13_ahead_out16_ab.log); the batch-end
+// remainder keeps the lane-granular stores.
 // Buffer resources sized to the valid bytes drop lanes past the end, so every
 // store issues and the vmcnt bookkeeping stays exact.
 template <bool kFilter, bool kRank>
@@ -260,10 +263,32 @@ __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
         P.hash ? (void *)(P.hash + t_first) : (void *)P.q, 0, P.hash ? (int)(nv * 4u) : 0,
         kRsrcWord3);
-    for (uint32_t j = 0; j < ntiles; ++j) {
-        const uint32_t e = j * kTile + lane;
-        __builtin_amdgcn_raw_buffer_store_b16(oq[e], rq, (int)(e * 2u), 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(oh[e], rh, (int)(e * 4u), 0, 0);
+    if (P.out16 && nv == ntiles * (uint32_t)kTile) {
+        // a whole batch of tiles: 16-byte stores, 1 KiB of hash and 512 B of
+        // q per wave-instruction at 4 tiles; out16 == 2 stores write-through
+        // (sc1: the lines leave L2 at once, none is left dirty at kernel end)
+        wave_lds_sync();
+        const uint32_t nh = nv >> 2, nq8 = nv >> 3;
+        const u32x4 vh = *reinterpret_cast<const u32x4 *>(oh + 4u * min(lane, nh - 1u));
+        const u32x4 vq = *reinterpret_cast<const u32x4 *>(oq + 8u * min(lane, nq8 - 1u));
+        if (P.out16 == 2) {
+            if (lane < nh)
+                __builtin_amdgcn_raw_buffer_store_b128(vh, rh, (int)(lane * 16u), 0, 16);
+            if (lane < nq8)
+                __builtin_amdgcn_raw_buffer_store_b128(vq, rq, (int)(lane * 16u), 0, 16);
+        } else {
+            if (lane < nh)
+                __builtin_amdgcn_raw_buffer_store_b128(vh, rh, (int)(lane * 16u), 0, 0);
+            if (lane < nq8)
+                __builtin_amdgcn_raw_buffer_store_b128(vq, rq, (int)(lane * 16u), 0, 0);
+        }
+        wave_lds_sync();
+    } else {
+        for (uint32_t j = 0; j < ntiles; ++j) {
+            const uint32_t e = j * kTile + lane;
+            __builtin_amdgcn_raw_buffer_store_b16(oq[e], rq, (int)(e * 2u), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(oh[e], rh, (int)(e * 4u), 0, 0);
+        }
     }
     if (kFilter) {
         const __amdgpu_buffer_rsrc_t rf =
@@ -2085,6 +2110,9 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         if (v >= 4 && v <= kMaxWavesPerCU)
             c->waves_per_cu = (uint32_t)v;
     }
+    c->proto.out16 = 2;   // 16-byte sc1 bursts (profiles/r01_v13_ahead_out16_ab.log)
+    if (const char *e = getenv("YRSS_OUT16"))
+        c->proto.out16 = (uint32_t)std::min(2, std::max(0, atoi(e)));
     if (const char *e = getenv("YRSS_NO_SMALL"))
         c->no_small = atoi(e) != 0;
     if (const char *e = getenv("YRSS_EVENT_FLAGS"))   // A/B of the timing-event fence
