@@ -220,3 +220,21 @@ def test_async_staged_and_frames(dev, oracle_mod):
         assert lib.yrss_wait(eng._ctx) == 0
         assert np.array_equal(oq, q) and np.array_equal(oh, h) and np.array_equal(oqi, qi)
         eng.unregister_host_memory(pool.ctypes.data)
+
+
+def test_async_python_wrapper(dev, oracle_mod):
+    """SoftRss.dispatch_burst(_zc)(async_=True) + wait() on two engines."""
+    cfg = (3, 3, 1, 1)
+    n = 2500
+    frames = _frames(oracle_mod, 2 * n, 321)
+    want = [_expect(oracle_mod, frames[:n], cfg), _expect(oracle_mod, frames[n:], cfg)]
+    pool, ptrs, _ = _fake_mbufs(frames)
+    with SoftRss(*cfg, device=0, max_burst=0) as e0, SoftRss(*cfg, device=0, max_burst=0) as e1:
+        r0 = e0.dispatch_burst(ptrs[:n], async_=True)
+        e1.register_host_memory(pool.ctypes.data, pool.nbytes)
+        r1 = e1.dispatch_burst_zc(ptrs[n:], async_=True)
+        e0.wait()
+        e1.wait()
+        _check(r0, *want[0])
+        _check(r1, *want[1])
+        e1.unregister_host_memory(pool.ctypes.data)

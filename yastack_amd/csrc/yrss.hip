@@ -2150,6 +2150,14 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         return hip_fail("yrss_init allocation", e);
     }
     *c->d_scan_fault = 0;
+    // The memsets above run on the null stream, which does not order against
+    // the context's non-blocking stream: without this wait a first dispatch
+    // could race the zeroing of the count matrix (seen once on the GPU box as
+    // short per-queue totals on a fresh context).
+    if ((e = hipDeviceSynchronize()) != hipSuccess) {
+        yrss_fini(c);
+        return hip_fail("yrss_init synchronize", e);
+    }
     if (cfg->max_burst && (rc = ensure_burst(c, cfg->max_burst)) != 0) {
         yrss_fini(c);
         return rc;
@@ -2213,6 +2221,7 @@ int yrss_set_kni(yrss_ctx *c, int enable, const char *method, const char *tcp_po
     c->kni_accept = accept;
     YRSS_HIP(hipSetDevice(c->device));
     YRSS_HIP(hipMemcpy(c->d_kni, c->kni_bm, sizeof(c->kni_bm), hipMemcpyHostToDevice));
+    YRSS_HIP(hipDeviceSynchronize());   // ordered before any stream's next dispatch
     return 0;
 }
 

@@ -189,19 +189,30 @@ class SoftRss:
                               None if qi is None else qi[:n], qs)
 
     def dispatch_burst(self, mbuf_ptrs: np.ndarray, want_hash=True, compact=True,
-                       write_rss=False) -> DispatchResult:
-        """Classify a burst of ``struct rte_mbuf *`` (uint64 addresses)."""
+                       write_rss=False, async_=False) -> DispatchResult:
+        """Classify a burst of ``struct rte_mbuf *`` (uint64 addresses).
+
+        ``async_=True`` (YRSS_F_ASYNC) returns once the burst is queued; the
+        result's arrays are valid after :meth:`wait`."""
         mb = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
         n = int(mb.size)
         q = np.empty(max(n, 1), np.int16)
         h = np.empty(max(n, 1), np.uint32) if want_hash else None
         qi = np.empty(max(n, 1), np.uint32) if compact else None
         qs = np.empty(self.nb_queues + 2, np.uint32) if compact else None
+        flags = (abi.F_WRITE_RSS if write_rss else 0) | (abi.F_ASYNC if async_ else 0)
         rc = self._lib.yrss_dispatch_burst(self._ctx, _ptr(mb), n, _ptr(q), _ptr(h), _ptr(qi),
-                                           _ptr(qs), abi.F_WRITE_RSS if write_rss else 0)
+                                           _ptr(qs), flags)
         abi.check(rc, "yrss_dispatch_burst")
+        self._inflight = mb if async_ else None   # keep the pointer array alive
         return DispatchResult(q[:n], None if h is None else h[:n],
                               None if qi is None else qi[:n], qs)
+
+    def wait(self) -> None:
+        """Complete the burst queued with ``async_=True`` (``yrss_wait``)."""
+        rc = self._lib.yrss_wait(self._ctx)
+        self._inflight = None
+        abi.check(rc, "yrss_wait")
 
     def register_host_memory(self, base: int, nbytes: int) -> None:
         abi.check(self._lib.yrss_register_host_memory(self._ctx, base, nbytes),
@@ -212,17 +223,20 @@ class SoftRss:
                   "yrss_unregister_host_memory")
 
     def dispatch_burst_zc(self, mbuf_ptrs: np.ndarray, want_hash=True, compact=True,
-                          write_rss=False) -> DispatchResult:
-        """Zero-copy burst: mbufs in registered host memory are read by the GPU."""
+                          write_rss=False, async_=False) -> DispatchResult:
+        """Zero-copy burst: mbufs in registered host memory are read by the GPU.
+        ``async_`` as in :meth:`dispatch_burst`."""
         mb = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
         n = int(mb.size)
         q = np.empty(max(n, 1), np.int16)
         h = np.empty(max(n, 1), np.uint32) if want_hash else None
         qi = np.empty(max(n, 1), np.uint32) if compact else None
         qs = np.empty(self.nb_queues + 2, np.uint32) if compact else None
+        flags = (abi.F_WRITE_RSS if write_rss else 0) | (abi.F_ASYNC if async_ else 0)
         rc = self._lib.yrss_dispatch_burst_zc(self._ctx, _ptr(mb), n, _ptr(q), _ptr(h), _ptr(qi),
-                                              _ptr(qs), abi.F_WRITE_RSS if write_rss else 0)
+                                              _ptr(qs), flags)
         abi.check(rc, "yrss_dispatch_burst_zc")
+        self._inflight = mb if async_ else None
         return DispatchResult(q[:n], None if h is None else h[:n],
                               None if qi is None else qi[:n], qs)
 
