@@ -395,3 +395,33 @@ def test_frames_zero_copy(dev, oracle_mod):
         assert a_q.tolist() == [x for x, _ in want] and a_h.tolist() == [y for _, y in want]
         eng.unregister_host_memory(arena.ctypes.data)
         eng.unregister_host_memory(pool.ctypes.data)
+
+
+def test_dispatch_across_streams(dev, oracle_mod):
+    """One context, back-to-back dispatches on two different streams and a host
+    burst on the context's own stream: the shared compaction workspace is
+    handed from stream to stream, so every result is exact."""
+    n = 1 << 20
+    with SoftRss(5, 4, 1, 1, device=0, max_burst=0) as eng:
+        win, lens = eng.synth(abi.SYN_FUZZ, n, 77, stride=80)
+        torch.cuda.synchronize()
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        o1 = eng.alloc_out(n, dev)
+        o2 = eng.alloc_out(n, dev)
+        for _ in range(3):
+            eng.dispatch_dev(win, lens, 80, out=o1, stream=s1)
+            eng.dispatch_dev(win, lens, 80, out=o2, stream=s2)
+        w_h = win.cpu().numpy()
+        l_h = to_np(lens[:n], np.uint16)
+        frames = [w_h[i * 80: i * 80 + min(int(l_h[i]), 80)].tobytes() for i in range(3000)]
+        r3 = eng.dispatch_frames(frames)        # host path, context stream
+        torch.cuda.synchronize()
+        c = oracle_mod.cfg(5, 4, 1, 1)
+        q_ref, h_ref = oracle_mod.dispatch_windows(w_h, 80, l_h, c)
+        qi_ref, qs_ref = oracle_mod.process_burst(q_ref, 4)
+        for o in (o1, o2):
+            assert np.array_equal(to_np(o.q[:n], np.int16), q_ref)
+            assert np.array_equal(to_np(o.qstart, np.uint32), qs_ref)
+            assert np.array_equal(to_np(o.qidx[:n], np.uint32), qi_ref)
+        want = [oracle_mod.toeplitz_dispatch(f, len(f), c)[0] for f in frames]
+        assert np.asarray(r3.q).tolist() == want

@@ -1541,6 +1541,13 @@ struct yrss_ctx {
     uint64_t *dh_ptrs = nullptr;
     uint32_t *dh_fault = nullptr;
     PendingBurst pend;
+    // The compaction workspace is shared by every dispatch of the context; a
+    // dispatch on a different stream than the previous one first waits for
+    // the work queued on that stream (recorded at the switch, so same-stream
+    // dispatches pay nothing).
+    hipStream_t last_stream = nullptr;
+    bool last_stream_valid = false;
+    hipEvent_t switch_ev = nullptr;
     // timing
     uint32_t timing_mask = 0;    // bit k: bracket kernel k with events
     std::vector<hipEvent_t> ev_free;
@@ -2145,7 +2152,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         (e = hipHostGetDevicePointer((void **)&c->dh_fault, c->h_fault, 0)) != hipSuccess ||
         (e = hipMemset(c->d_kni, 0, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipMemset(c->d_seg_cnt, 0, ws)) != hipSuccess ||
-        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) {
+        (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming)) != hipSuccess) {
         yrss_fini(c);
         return hip_fail("yrss_init allocation", e);
     }
@@ -2172,8 +2180,9 @@ void yrss_fini(yrss_ctx *c)
         return;
     (void)hipSetDevice(c->device);
     c->pend.active = false;   // its outputs are abandoned with the context
-    if (c->stream)
-        (void)hipStreamSynchronize(c->stream);
+    // device dispatches may still run on the caller's streams: drain the
+    // device before the workspace goes
+    (void)hipDeviceSynchronize();
     for (auto &p : c->ev_pending) {
         (void)hipEventDestroy(p.a);
         (void)hipEventDestroy(p.b);
@@ -2192,6 +2201,8 @@ void yrss_fini(yrss_ctx *c)
     (void)hipHostFree(c->h_fault);
     for (uint32_t r = 0; r < c->nranges; ++r)
         host_reg_release(c->range_base[r]);
+    if (c->switch_ev)
+        (void)hipEventDestroy(c->switch_ev);
     if (c->stream)
         (void)hipStreamDestroy(c->stream);
     delete c;
@@ -2259,6 +2270,12 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         return 0;
     }
 
+    if (c->last_stream_valid && c->last_stream != s) {
+        YRSS_HIP(hipEventRecord(c->switch_ev, c->last_stream));
+        YRSS_HIP(hipStreamWaitEvent(s, c->switch_ev, 0));
+    }
+    c->last_stream = s;
+    c->last_stream_valid = true;
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
     // 18..65 buckets (16-tile chunks): the parse kernel also emits each
