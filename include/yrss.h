@@ -144,7 +144,11 @@ void yrss_fini(yrss_ctx *ctx);
  *              ff_dpdk_if.c:1080-1083).  Bucket b = d_qidx[d_qstart[b] ..
  *              d_qstart[b+1]).  d_qstart[nb_queues+1] == n.
  *   stream     hipStream_t (NULL = legacy default stream)
- * n <= YRSS_MAX_BATCH.  Asynchronous: returns after enqueueing the kernels. */
+ * n <= YRSS_MAX_BATCH.  Asynchronous: returns after enqueueing the kernels.
+ * Dispatches of one context share its compaction workspace: a dispatch on a
+ * different stream than the context's previous one waits (on the device) for
+ * the work already queued there, so streams may be mixed freely; dispatches
+ * on one stream pay nothing for this.  yrss_fini drains the device. */
 int yrss_dispatch_dev(yrss_ctx *ctx, const uint8_t *d_win, uint32_t win_stride,
                       const uint16_t *d_len, uint32_t n, int16_t *d_q,
                       uint32_t *d_hash, uint32_t *d_qidx, uint32_t *d_qstart,
