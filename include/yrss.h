@@ -368,6 +368,37 @@ int yrss_timing_enable(yrss_ctx *ctx, int kernel_mask);
 int yrss_timing_read(yrss_ctx *ctx, int kernel, double *total_ms,
                      uint32_t *launches);
 
+/* ---- persistent burst worker ------------------------------------------------------ */
+
+/* Small bursts with no kernel launch and no stream synchronisation per burst:
+ * a persistent gfx950 kernel (nblocks workgroups, one CU each) polls a ring of
+ * nslots slots in host-coherent pinned memory.  Submit copies the mbuf pointer
+ * array into a slot and publishes it; the kernel reads the mbufs (which must
+ * lie in memory registered with yrss_register_host_memory) over PCIe,
+ * classifies them like yrss_dispatch_burst_zc and writes the results into the
+ * slot; poll copies them to the caller's arrays.  Up to nslots bursts are in
+ * flight; every ticket must be polled before its slot is reused (submit
+ * returns -EBUSY otherwise).  The kernel leaves after YRSS_WORKER_IDLE_MS
+ * (default 50) without work or YRSS_WORKER_LIFE_MS (default 1000) in total and
+ * is relaunched transparently by the next submit or poll; registering or
+ * unregistering host memory restarts it.  nslots is a multiple of nblocks;
+ * nb_queues + 1 <= 64. */
+#define YRSS_WORKER_MAX_BURST 1024
+#define YRSS_WORKER_MAX_BLOCKS 32
+#define YRSS_WORKER_MAX_SLOTS 4096
+int yrss_worker_start(yrss_ctx *ctx, uint32_t nslots, uint32_t nblocks);
+/* Queue one burst (n <= YRSS_WORKER_MAX_BURST; flags: YRSS_F_WRITE_RSS);
+ * *ticket identifies it for yrss_worker_poll.  The output arrays must stay
+ * valid until the ticket is polled. */
+int yrss_worker_submit(yrss_ctx *ctx, void *const *mbufs, uint32_t n, int16_t *out_q,
+                       uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                       uint32_t flags, uint64_t *ticket);
+/* 0: the burst is done and its outputs copied; -EAGAIN: not yet (wait = 0);
+ * -EFAULT: a mbuf or its data lies outside every registered range. */
+int yrss_worker_poll(yrss_ctx *ctx, uint64_t ticket, int wait);
+/* Stop the kernel and free the ring (also done by yrss_fini). */
+int yrss_worker_stop(yrss_ctx *ctx);
+
 /* ---- device-side status ----------------------------------------------------------- */
 
 /* Synchronises the device and reports (then clears) a device-side fault of an

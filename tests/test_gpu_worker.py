@@ -1,0 +1,117 @@
+"""GPU parity of the persistent burst worker (yrss_worker_*): bursts handed
+to a resident gfx950 kernel through a ring in host-coherent memory, checked
+against the oracle; relaunch after an idle exit; fault and limit reporting.
+"""
+import time
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from yastack_amd import SoftRss, abi  # noqa: E402
+
+from test_gpu_parity import _fake_mbufs  # noqa: E402
+from test_gpu_small_burst import _check, _expect, _frames  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("nslots,nblocks", [(16, 4), (8, 1), (32, 8)])
+def test_worker_bursts_vs_oracle(dev, oracle_mod, nslots, nblocks):
+    cfg = (5, 4, 1, 1)
+    rng = np.random.default_rng(nslots * 100 + nblocks)
+    sizes = [1, 32, 1024, 0, 33, 64, 1000, 7] + list(rng.integers(1, 1025, 30))
+    total = int(sum(sizes))
+    frames = _frames(oracle_mod, total, 4000 + nslots)
+    pool, ptrs, stride = _fake_mbufs(frames, headroom=129)
+    q_all, h_all, _, _ = _expect(oracle_mod, frames, cfg)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(nslots, nblocks)
+        tickets, offs, off = [], [], 0
+        for i, n in enumerate(sizes):
+            if len(tickets) - len(offs) >= 0 and i >= nslots:   # keep <= nslots in flight
+                _verify(eng, oracle_mod, tickets, offs, sizes, q_all, h_all, cfg)
+            tickets.append(eng.worker_submit(ptrs[off:off + n], write_rss=(i % 3 == 0)))
+            offs.append(off)
+            off += n
+        while len(offs) > 0 and tickets:
+            _verify(eng, oracle_mod, tickets, offs, sizes, q_all, h_all, cfg)
+        rss = pool.reshape(-1, stride)[:, 44:48].copy().view(np.uint32).ravel()
+        off = 0
+        for i, n in enumerate(sizes):
+            if i % 3 == 0 and n:
+                assert np.array_equal(rss[off:off + n], h_all[off:off + n])
+            off += n
+        eng.worker_stop()
+        eng.unregister_host_memory(pool.ctypes.data)
+
+
+def _verify(eng, oracle_mod, tickets, offs, sizes, q_all, h_all, cfg):
+    t = tickets.pop(0)
+    off = offs.pop(0)
+    n = sizes[t - 1]
+    r = eng.worker_poll(t)
+    q = q_all[off:off + n]
+    qi, qs = oracle_mod.process_burst(q, cfg[1])
+    _check(r, q, h_all[off:off + n], qi, qs)
+
+
+def test_worker_idle_exit_and_relaunch(dev, oracle_mod, monkeypatch):
+    monkeypatch.setenv("YRSS_WORKER_IDLE_MS", "5")
+    monkeypatch.setenv("YRSS_WORKER_LIFE_MS", "200")
+    cfg = (3, 3, 1, 1)
+    frames = _frames(oracle_mod, 600, 9)
+    pool, ptrs, _ = _fake_mbufs(frames)
+    q, h, _, _ = _expect(oracle_mod, frames, cfg)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(4, 2)
+        for k in range(6):
+            lo = 100 * k
+            t = eng.worker_submit(ptrs[lo:lo + 100])
+            r = eng.worker_poll(t)
+            qi, qs = oracle_mod.process_burst(q[lo:lo + 100], 3)
+            _check(r, q[lo:lo + 100], h[lo:lo + 100], qi, qs)
+            time.sleep(0.03 if k % 2 == 0 else 0.25)   # past the idle / lifetime limits
+        # registering more memory restarts the worker with the new range table
+        extra = _frames(oracle_mod, 50, 10)
+        pool2, ptrs2, _ = _fake_mbufs(extra)
+        eng.register_host_memory(pool2.ctypes.data, pool2.nbytes)
+        q2, h2, qi2, qs2 = _expect(oracle_mod, extra, cfg)
+        _check(eng.worker_poll(eng.worker_submit(ptrs2)), q2, h2, qi2, qs2)
+        eng.worker_stop()
+        eng.unregister_host_memory(pool2.ctypes.data)
+        eng.unregister_host_memory(pool.ctypes.data)
+
+
+def test_worker_errors(dev, oracle_mod):
+    cfg = (3, 3, 1, 1)
+    frames = _frames(oracle_mod, 1100, 12)
+    pool, ptrs, _ = _fake_mbufs(frames)
+    lib = abi.load()
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        assert lib.yrss_worker_start(eng._ctx, 6, 4) == -22          # nslots % nblocks
+        assert lib.yrss_worker_start(eng._ctx, 4, 64) == -22         # too many blocks
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(2, 1)
+        with pytest.raises(abi.YrssError):
+            eng.worker_submit(ptrs[:1025])                            # > 1024 packets
+        bad = ptrs[:50].copy()
+        bad[7] = np.uint64(pool.ctypes.data + pool.nbytes + 8192)
+        tb = eng.worker_submit(bad)
+        t2 = eng.worker_submit(ptrs[:20])
+        with pytest.raises(abi.YrssError):
+            eng.worker_submit(ptrs[:5])                               # both slots unpolled
+        with pytest.raises(abi.YrssError):
+            eng.worker_poll(tb)                                       # -EFAULT
+        q, h, qi, qs = _expect(oracle_mod, frames[:20], cfg)
+        _check(eng.worker_poll(t2), q, h, qi, qs)
+        eng.worker_stop()
+        eng.unregister_host_memory(pool.ctypes.data)

@@ -49,6 +49,82 @@ static double now(void)
     return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
+/* Persistent worker (yrss_worker_*): `depth` bursts in flight through the
+ * ring; the oldest is polled before a slot is reused. */
+static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_sz,
+                      uint8_t *arena, size_t arena_sz, void **mbufs, uint32_t pool, uint32_t B,
+                      double secs, int16_t *q_all, uint32_t *h_all, uint32_t *qi_all,
+                      uint32_t profile, int thp)
+{
+    const char *de = getenv("YRSS_CBENCH_WORKER_DEPTH");
+    const char *be = getenv("YRSS_CBENCH_WORKER_BLOCKS");
+    unsigned blocks = be ? (unsigned)atoi(be) : 4u;
+    unsigned depth = de ? (unsigned)atoi(de) : 16u;
+    if (blocks < 1 || blocks > YRSS_WORKER_MAX_BLOCKS)
+        blocks = 4;
+    if (depth < blocks)
+        depth = blocks;
+    depth = (depth + blocks - 1) / blocks * blocks;
+    if ((uint64_t)depth * B > pool || B > YRSS_WORKER_MAX_BURST)
+        return 0;
+    struct yrss_config cfg = *cfg0;
+    cfg.max_burst = 0;
+    yrss_ctx *ctx = NULL;
+    int rc;
+    if ((rc = yrss_init(&cfg, &ctx)) || (rc = yrss_register_host_memory(ctx, mem, mem_sz)) ||
+        (rc = yrss_register_host_memory(ctx, arena, arena_sz)) ||
+        (rc = yrss_worker_start(ctx, depth, blocks))) {
+        fprintf(stderr, "worker setup: %d\n", rc);
+        return 2;
+    }
+    static uint32_t qs[YRSS_WORKER_MAX_SLOTS][YRSS_MAX_QUEUES + 2];
+    uint64_t *tk = calloc(depth, sizeof(uint64_t));
+    uint64_t pkts = 0, i = 0;
+    uint32_t off = 0;
+    double t0 = 0, t1 = 0;
+    for (int pass = 0; pass < 2; ++pass) {          /* pass 0: warm-up */
+        const double lim = pass ? secs : 0.2;
+        t0 = now();
+        t1 = t0;
+        pkts = 0;
+        while (t1 - t0 < lim) {
+            if (off + B > pool)
+                off = 0;
+            const unsigned k = (unsigned)(i % depth);
+            if (i >= depth && (rc = yrss_worker_poll(ctx, tk[k], 1)) != 0) {
+                fprintf(stderr, "worker poll: %d\n", rc);
+                return 3;
+            }
+            if ((rc = yrss_worker_submit(ctx, mbufs + off, B, q_all + off, h_all + off,
+                                         qi_all + off, qs[k], 0, &tk[k])) != 0) {
+                fprintf(stderr, "worker submit: %d\n", rc);
+                return 3;
+            }
+            ++i;
+            off += B;
+            pkts += B;
+            t1 = now();
+        }
+    }
+    for (uint64_t j = i > depth ? i - depth : 0; j < i; ++j)
+        if ((rc = yrss_worker_poll(ctx, tk[j % depth], 1)) != 0) {
+            fprintf(stderr, "worker poll: %d\n", rc);
+            return 3;
+        }
+    t1 = now();
+    printf("{\"tool\": \"yrss_cbench\", \"api\": \"yrss_worker\", \"profile\": %u, "
+           "\"burst\": %u, \"inflight\": %u, \"blocks\": %u, \"pkts\": %llu, "
+           "\"seconds\": %.3f, \"mpps\": %.2f, \"us_per_burst\": %.2f, \"thp\": %d, "
+           "\"mode\": 4, \"note\": \"persistent kernel polls a ring of bursts in pinned "
+           "memory; mbufs read over PCIe\"}\n",
+           profile, B, depth, blocks, (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
+           (t1 - t0) / (pkts / (double)B) * 1e6, thp);
+    fflush(stdout);
+    free(tk);
+    yrss_fini(ctx);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     const uint32_t profile = argc > 1 ? (uint32_t)atoi(argv[1]) : YRSS_SYN_UDP4;
@@ -212,6 +288,16 @@ int main(int argc, char **argv)
         if (burst_arg)
             break;
     }
+    if (mode_env && strchr(mode_env, '4'))
+        for (unsigned bi = 0; bi < 2; ++bi) {
+            const uint32_t B = burst_arg ? burst_arg : bursts[bi];
+            const int rc = run_worker(&cfg, mem, mem_sz, arena, arena_sz, mbufs, pool, B, secs,
+                                      q_all, h_all, qi_all, profile, thp);
+            if (rc)
+                return rc;
+            if (burst_arg)
+                break;
+        }
     free(arena);
     return 0;
 }

@@ -1160,27 +1160,44 @@ __device__ __forceinline__ uint32_t quad_word(const u32x4 &hv, uint32_t lane, ui
 // stride 80 and G.len.  kB iterations run in lockstep phases (pointers, then
 // headers, then data), so a wave has kB x 16 packets' PCIe reads in flight
 // per dependent step instead of 16.
+// The per-call pointers of a gather, apart from the range table and the mbuf
+// layout (GatherParams), so a persistent caller can vary them per burst
+// without copying the table.
+struct GatherIO {
+    const uint64_t *ptrs;
+    const uint16_t *lens;
+    uint8_t *win;
+    uint16_t *len;
+    uint32_t *fault;
+    uint32_t n;
+};
+
+__device__ __forceinline__ GatherIO gather_io(const GatherParams &G)
+{
+    return GatherIO{G.ptrs, G.lens, G.win, G.len, G.fault, G.n};
+}
+
 template <int kB>
-__device__ __forceinline__ void gather_quads(const GatherParams &G, uint32_t wave,
-                                             uint32_t nwaves, uint32_t lane)
+__device__ __forceinline__ void gather_quads(const GatherParams &G, const GatherIO &io,
+                                             uint32_t wave, uint32_t nwaves, uint32_t lane)
 {
     const uint32_t c = lane & 3u;
-    for (uint32_t p0 = wave * 16u * kB; p0 < G.n; p0 += nwaves * 16u * kB) {
+    for (uint32_t p0 = wave * 16u * kB; p0 < io.n; p0 += nwaves * 16u * kB) {
         uint32_t idx[kB], L[kB];
         uint64_t m[kB], data[kB];
         bool ok_m[kB];
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
             idx[k] = p0 + 16u * k + (lane >> 2);
-            m[k] = idx[k] < G.n ? G.ptrs[idx[k]] : 0u;
-            L[k] = (G.frames && idx[k] < G.n) ? G.lens[idx[k]] : 0u;
+            m[k] = idx[k] < io.n ? io.ptrs[idx[k]] : 0u;
+            L[k] = (G.frames && idx[k] < io.n) ? io.lens[idx[k]] : 0u;
         }
         if (G.frames) {
             // frames mode: the host already knows data pointer and data_len
 #pragma unroll
             for (int k = 0; k < kB; ++k) {
                 data[k] = m[k];
-                ok_m[k] = idx[k] < G.n;
+                ok_m[k] = idx[k] < io.n;
             }
         } else {
             u32x4 hv[kB];
@@ -1188,7 +1205,7 @@ __device__ __forceinline__ void gather_quads(const GatherParams &G, uint32_t wav
 #pragma unroll
             for (int k = 0; k < kB; ++k) {
                 dm[k] = 0;
-                ok_m[k] = idx[k] < G.n && host_xlate(G, m[k], 64u, &dm[k]);
+                ok_m[k] = idx[k] < io.n && host_xlate(G, m[k], 64u, &dm[k]);
                 hv[k] = u32x4{0u, 0u, 0u, 0u};
                 if (ok_m[k])
                     hv[k] = host_load16(m[k] + dm[k] + 16u * c);
@@ -1220,15 +1237,15 @@ __device__ __forceinline__ void gather_quads(const GatherParams &G, uint32_t wav
         }
 #pragma unroll
         for (int k = 0; k < kB; ++k) {
-            if (idx[k] >= G.n)
+            if (idx[k] >= io.n)
                 continue;
-            uint8_t *dst = G.win + (size_t)idx[k] * YRSS_WIN_FULL;
+            uint8_t *dst = io.win + (size_t)idx[k] * YRSS_WIN_FULL;
             *reinterpret_cast<u32x4 *>(dst + 16u * c) = w[k];
             if (c == 0) {
                 *reinterpret_cast<u32x4 *>(dst + 64u) = t[k];
-                G.len[idx[k]] = (uint16_t)L[k];
+                io.len[idx[k]] = (uint16_t)L[k];
                 if (!ok_d[k])   // plain store: the word may live in host memory
-                    __hip_atomic_store(G.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(io.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
     }
@@ -1237,7 +1254,7 @@ __device__ __forceinline__ void gather_quads(const GatherParams &G, uint32_t wav
 __global__ __launch_bounds__(256) void yrss_gather_zc(GatherParams G)
 {
     const uint32_t wave = (blockIdx.x * 256u + threadIdx.x) / kWave;
-    gather_quads<1>(G, wave, gridDim.x * (256u / kWave), lane_id());
+    gather_quads<1>(G, gather_io(G), wave, gridDim.x * (256u / kWave), lane_id());
 }
 
 // hash.rss write-back straight into the host mbufs (YRSS_F_WRITE_RSS)
@@ -1289,49 +1306,81 @@ struct SmallParams {
     uint32_t writeback;  // 1: store hash.rss into each mbuf (YRSS_F_WRITE_RSS)
 };
 
-size_t small_lds(uint32_t nb, bool filter)
+__host__ __device__ inline size_t small_lds(uint32_t nb, bool filter)
 {
     return kTblBytes + kSmallWaves * (kStageBytes + kOutBytes) +
            (size_t)(kSmallTiles * nb + kSmallMaxNb) * sizeof(uint32_t) +
            (filter ? kKniWords * sizeof(uint32_t) : 0u);
 }
 
-template <bool kFilter>
-__global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
-{
-    const ParseParams &P = S.P;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint32_t lane = lane_id();
-    uint32_t *tbl = reinterpret_cast<uint32_t *>(smem);
-    u32x4 *stage = reinterpret_cast<u32x4 *>(smem + kTblBytes + wave * kStageBytes);
-    uint8_t *out_w = smem + kTblBytes + kSmallWaves * kStageBytes + wave * kOutBytes;
-    uint32_t *oh = reinterpret_cast<uint32_t *>(out_w);
-    uint16_t *oq = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 4);
-    int8_t *of = reinterpret_cast<int8_t *>(out_w + kOutTiles * kTile * 6);
-    uint16_t *orank = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 7);
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(smem + kTblBytes +
-                                                 kSmallWaves * (kStageBytes + kOutBytes));
-    uint32_t *start = cnt + kSmallTiles * P.nb;
-    uint32_t *kni = start + kSmallMaxNb;
+// LDS carve-up shared by the one-shot kernel and the worker.
+struct SmallLds {
+    uint32_t *tbl;
+    u32x4 *stage;
+    uint32_t *oh;
+    uint16_t *oq;
+    int8_t *of;
+    uint16_t *orank;
+    uint32_t *cnt;
+    uint32_t *start;
+    uint32_t *kni;
+};
 
-    // wave w owns tiles w, w + 16, w + 32, w + 48: with 4 lockstep rounds of
-    // 16 packets, gather_quads' wave-iteration p0 = 64 (w + 16 j) is tile j's
-    if (S.gather)
-        gather_quads<4>(S.G, wave, kSmallWaves, lane);
+__device__ __forceinline__ SmallLds small_carve(uint8_t *smem, uint32_t wave, uint32_t nb)
+{
+    SmallLds L;
+    L.tbl = reinterpret_cast<uint32_t *>(smem);
+    L.stage = reinterpret_cast<u32x4 *>(smem + kTblBytes + wave * kStageBytes);
+    uint8_t *out_w = smem + kTblBytes + kSmallWaves * kStageBytes + wave * kOutBytes;
+    L.oh = reinterpret_cast<uint32_t *>(out_w);
+    L.oq = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 4);
+    L.of = reinterpret_cast<int8_t *>(out_w + kOutTiles * kTile * 6);
+    L.orank = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 7);
+    L.cnt = reinterpret_cast<uint32_t *>(smem + kTblBytes +
+                                         kSmallWaves * (kStageBytes + kOutBytes));
+    L.start = L.cnt + kSmallTiles * nb;
+    L.kni = L.start + kSmallMaxNb;
+    return L;
+}
+
+// Byte tables (and KNI bitmaps) for the workgroup; the caller synchronises.
+template <bool kFilter>
+__device__ __forceinline__ void small_tables(const ParseParams &P, const SmallLds &L)
+{
     for (uint32_t e = threadIdx.x; e < 12u * 256u; e += kSmallBlock) {
         const uint32_t jt = e >> 8, v = e & 255u;
         uint32_t acc = 0;
 #pragma unroll
         for (int b = 0; b < 8; ++b)
             acc ^= (v & (0x80u >> b)) ? P.kwin[8 * jt + b] : 0u;
-        tbl[e] = acc;
+        L.tbl[e] = acc;
     }
     if (kFilter)
         for (uint32_t e = threadIdx.x; e < (uint32_t)kKniWords; e += kSmallBlock)
-            kni[e] = P.kni_enable ? P.kni_bm[e] : 0u;
+            L.kni[e] = P.kni_enable ? P.kni_bm[e] : 0u;
+}
+
+// One burst through one workgroup, tables already in LDS: gather (zero-copy
+// modes), parse, per-bucket FIFO lists, outputs to host-visible memory.
+// Per-burst outputs and switches of small_burst_body.
+struct BurstIO {
+    uint32_t *qidx;      // host-visible, or null
+    uint32_t *qstart;    // host-visible [nb + 1], or null
+    uint32_t gather;     // 1: gather the windows first (zero-copy modes)
+    uint32_t writeback;  // 1: store hash.rss into each mbuf (YRSS_F_WRITE_RSS)
+};
+
+template <bool kFilter, uint32_t kTW = kOutTiles>   // kTW: tiles per wave (n <= kTW * 1024)
+__device__ void small_burst_body(const ParseParams &P, const GatherParams &G, const GatherIO &gio,
+                                 const BurstIO &S, const SmallLds &L, uint32_t wave,
+                                 uint32_t lane)
+{
+    // wave w owns tiles w, w + 16, w + 32, w + 48: with 4 lockstep rounds of
+    // 16 packets, gather_quads' wave-iteration p0 = 64 (w + 16 j) is tile j's
+    if (S.gather)
+        gather_quads<4>(G, gio, wave, kSmallWaves, lane);
     for (uint32_t e = threadIdx.x; e < kSmallTiles * P.nb; e += kSmallBlock)
-        cnt[e] = 0;
+        L.cnt[e] = 0;
     // also orders the gathered windows (global scratch written by this
     // workgroup) before the parse reads them
     __syncthreads();
@@ -1339,22 +1388,22 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
     const uint32_t ntiles = (P.n + kTile - 1) / kTile;
     // all of the wave's tiles are loaded before the first is parsed: the
     // windows may sit in host memory, one PCIe round trip for all of them
-    u32x4 r[kOutTiles][4];
-    uint32_t L[kOutTiles];
+    u32x4 r[kTW][4];
+    uint32_t Ln[kTW];
 #pragma unroll
-    for (uint32_t j = 0; j < kOutTiles; ++j) {
+    for (uint32_t j = 0; j < kTW; ++j) {
         const uint32_t t = min(wave + j * kSmallWaves, ntiles - 1u);
-        load_tile<false>(P, t * kTile, P.n, lane, r[j], L[j]);
+        load_tile<false>(P, t * kTile, P.n, lane, r[j], Ln[j]);
     }
 #pragma unroll
-    for (uint32_t j = 0; j < kOutTiles; ++j) {
+    for (uint32_t j = 0; j < kTW; ++j) {
         const uint32_t t = wave + j * kSmallWaves;
         if (t >= ntiles)
             break;
-        process_tile<2, kFilter>(P, tbl, kni, stage, cnt + t * P.nb,
-                                 OutSlot{oq + j * kTile, oh + j * kTile, of + j * kTile,
-                                         orank + j * kTile},
-                                 t * kTile, P.n, lane, r[j], L[j]);
+        process_tile<2, kFilter>(P, L.tbl, L.kni, L.stage, L.cnt + t * P.nb,
+                                 OutSlot{L.oq + j * kTile, L.oh + j * kTile, L.of + j * kTile,
+                                         L.orank + j * kTile},
+                                 t * kTile, P.n, lane, r[j], Ln[j]);
     }
     __syncthreads();
     // per bucket: exclusive prefix over the tiles (in place) and the total
@@ -1362,18 +1411,18 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
         const uint32_t b = threadIdx.x;
         uint32_t run = 0;
         for (uint32_t t = 0; t < ntiles; ++t) {
-            const uint32_t v = cnt[t * P.nb + b];
-            cnt[t * P.nb + b] = run;
+            const uint32_t v = L.cnt[t * P.nb + b];
+            L.cnt[t * P.nb + b] = run;
             run += v;
         }
-        start[b] = run;
+        L.start[b] = run;
     }
     __syncthreads();
     if (wave == 0) {
-        const uint32_t tot = lane < P.nb ? start[lane] : 0u;
+        const uint32_t tot = lane < P.nb ? L.start[lane] : 0u;
         const uint32_t x = wave_incl_scan(tot, lane);
         if (lane < P.nb) {
-            start[lane] = x - tot;
+            L.start[lane] = x - tot;
             if (S.qstart)
                 S.qstart[lane] = x - tot;
         }
@@ -1381,27 +1430,172 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
             S.qstart[P.nb] = x;
     }
     __syncthreads();
-    for (uint32_t j = 0; j < kOutTiles; ++j) {
+    for (uint32_t j = 0; j < kTW; ++j) {
         const uint32_t t = wave + j * kSmallWaves;
         if (t >= ntiles)
             break;
-        flush_out<kFilter, false>(P, oq + j * kTile, oh + j * kTile, of + j * kTile,
-                                  orank + j * kTile, t * kTile, 1u, lane);
+        flush_out<kFilter, false>(P, L.oq + j * kTile, L.oh + j * kTile, L.of + j * kTile,
+                                  L.orank + j * kTile, t * kTile, 1u, lane);
         const uint32_t pkt = t * kTile + lane;
         if (pkt < P.n) {
             if (S.qidx) {
-                const uint32_t b = bucket_of((int16_t)oq[j * kTile + lane], P.nq);
-                S.qidx[start[b] + cnt[t * P.nb + b] + orank[j * kTile + lane]] = pkt;
+                const uint32_t b = bucket_of((int16_t)L.oq[j * kTile + lane], P.nq);
+                S.qidx[L.start[b] + L.cnt[t * P.nb + b] + L.orank[j * kTile + lane]] = pkt;
             }
             if (S.writeback) {
-                const uint64_t m = S.G.ptrs[pkt];
+                const uint64_t m = gio.ptrs[pkt];
                 int64_t dm = 0;
-                if (host_xlate(S.G, m, S.G.off_hash_rss + 4u, &dm))
-                    *reinterpret_cast<uint32_t *>(m + dm + S.G.off_hash_rss) =
-                        oh[j * kTile + lane];
+                if (host_xlate(G, m, G.off_hash_rss + 4u, &dm))
+                    *reinterpret_cast<uint32_t *>(m + dm + G.off_hash_rss) =
+                        L.oh[j * kTile + lane];
             }
         }
     }
+}
+
+template <bool kFilter>
+__global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const SmallLds L = small_carve(smem, wave, S.P.nb);
+    small_tables<kFilter>(S.P, L);
+    small_burst_body<kFilter>(S.P, S.G, gather_io(S.G),
+                              BurstIO{S.qidx, S.qstart, S.gather, S.writeback}, L, wave,
+                              lane_id());
+}
+
+// ---------------------------------------------------------------------------
+// Persistent burst worker (yrss_worker_*): no launch and no stream
+// synchronisation per burst.  The host writes a burst's mbuf pointers into a
+// slot of a ring in host-coherent pinned memory and publishes its ticket in
+// the slot's seq word; workgroup b of this kernel owns tickets b, b + B,
+// b + 2B, ... (B workgroups; slot = ticket mod nslots, nslots a multiple of
+// B), polls the seq word of its next ticket, runs the burst through
+// small_burst_body() (tables stay in LDS across bursts), writes q / hash /
+// lists into the slot's pinned output area and publishes the ticket in the
+// slot's done word.  Every workgroup leaves when the host sets the stop word,
+// after idle_ticks without work, or after life_ticks in total, storing the
+// ticket it would have served next; the host relaunches on the next submit.
+// Protocol (host-coherent memory, system scope): the host writes ptrs / n /
+// flags, then seq with release; the GPU polls seq relaxed, then acquires.
+// The GPU drains every wave's output stores (vmcnt(0) + barrier), releases
+// at system scope, then writes done; the host reads done with acquire.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kWorkerMaxBurst = YRSS_WORKER_MAX_BURST;   // 16 tiles: one per wave
+
+struct alignas(64) WorkerSlot {
+    uint64_t seq;        // host: ticket, written last (release)
+    uint64_t done;       // GPU: ticket, written after the outputs (release, system)
+    uint32_t n;
+    uint32_t flags;      // YRSS_F_WRITE_RSS
+    uint32_t fault;      // GPU: a pointer outside every registered range
+    uint32_t pad_[9];
+};
+static_assert(sizeof(WorkerSlot) == 64, "one line per slot header");
+
+struct WorkerParams {
+    ParseParams P;       // configuration (per-burst fields set in the kernel)
+    GatherParams G;      // range table and mbuf layout
+    WorkerSlot *slots;   // [nslots] host-coherent
+    uint64_t *ptrs;      // [nslots][kWorkerMaxBurst] pinned
+    int16_t *q;          // [nslots][kWorkerMaxBurst] pinned outputs
+    uint32_t *hash;
+    uint32_t *qidx;
+    uint32_t *qstart;    // [nslots][qs_stride]
+    uint8_t *win;        // device scratch [nblocks][kWorkerMaxBurst * 80]
+    uint16_t *len;       // device scratch [nblocks][kWorkerMaxBurst]
+    uint64_t *next;      // host-coherent [nblocks]: ticket to serve next (resume)
+    uint32_t *stop;      // host-coherent stop word
+    uint32_t nslots;
+    uint32_t qs_stride;
+    uint64_t idle_ticks; // s_memrealtime ticks (100 MHz)
+    uint64_t life_ticks;
+};
+
+size_t worker_lds(uint32_t nb) { return small_lds(nb, false) + 64u; }
+
+__global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const uint32_t lane = lane_id();
+    const SmallLds L = small_carve(smem, wave, W.P.nb);
+    uint32_t *ctl = reinterpret_cast<uint32_t *>(smem + small_lds(W.P.nb, false));
+    small_tables<false>(W.P, L);
+
+    uint64_t t = __hip_atomic_load(W.next + blockIdx.x, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t t_begin = wall_clock64();
+    uint64_t t_last = t_begin;
+    for (;;) {
+        const uint32_t si = (uint32_t)(t % W.nslots);
+        WorkerSlot *sl = W.slots + si;
+        if (threadIdx.x == 0) {
+            uint32_t go = 0;   // 1: a burst, 2: leave
+            for (;;) {
+                if (__hip_atomic_load(&sl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
+                    t) {
+                    go = 1;
+                    break;
+                }
+                const uint64_t now = wall_clock64();
+                if (__hip_atomic_load(W.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                    now - t_last > W.idle_ticks || now - t_begin > W.life_ticks) {
+                    go = 2;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (go == 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                ctl[1] = __hip_atomic_load(&sl->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                ctl[2] = __hip_atomic_load(&sl->flags, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&sl->fault, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            ctl[0] = go;
+        }
+        __syncthreads();
+        if (ctl[0] != 1u)
+            break;
+        const uint32_t n = min(ctl[1], kWorkerMaxBurst);
+        ParseParams P = W.P;
+        P.n = n;
+        P.win = W.win + (size_t)blockIdx.x * kWorkerMaxBurst * YRSS_WIN_FULL;
+        P.len = W.len + (size_t)blockIdx.x * kWorkerMaxBurst;
+        P.stride = YRSS_WIN_FULL;
+        P.q = W.q + (size_t)si * kWorkerMaxBurst;
+        P.hash = W.hash + (size_t)si * kWorkerMaxBurst;
+        P.filter = nullptr;
+        P.rank = nullptr;
+        P.seg_cnt = nullptr;
+        P.out16 = 0;
+        const GatherIO gio{W.ptrs + (size_t)si * kWorkerMaxBurst, nullptr,
+                           const_cast<uint8_t *>(P.win), const_cast<uint16_t *>(P.len),
+                           &sl->fault, n};
+        if (n) {
+            small_burst_body<false, 1>(P, W.G, gio,
+                                    BurstIO{W.qidx + (size_t)si * kWorkerMaxBurst,
+                                            W.qstart + (size_t)si * W.qs_stride, 1u,
+                                            (ctl[2] & YRSS_F_WRITE_RSS) ? 1u : 0u},
+                                    L, wave, lane);
+        } else if (threadIdx.x <= W.P.nb) {
+            W.qstart[(size_t)si * W.qs_stride + threadIdx.x] = 0u;
+        }
+        // every wave's output stores drained, then one system-scope release
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&sl->done, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        t_last = wall_clock64();
+        t += gridDim.x;
+    }
+    if (threadIdx.x == 0)
+        __hip_atomic_store(W.next + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -1541,6 +1735,31 @@ struct yrss_ctx {
     uint64_t *dh_ptrs = nullptr;
     uint32_t *dh_fault = nullptr;
     PendingBurst pend;
+    // persistent burst worker (yrss_worker_*)
+    struct WorkerState {
+        bool on = false;           // yrss_worker_start called
+        bool running = false;      // a worker launch may still be in flight
+        uint32_t nslots = 0, nblocks = 0, qs_stride = 0;
+        uint64_t idle_ticks = 0, life_ticks = 0;
+        hipStream_t stream = nullptr;
+        WorkerSlot *slots = nullptr, *d_slots = nullptr;   // host-coherent
+        uint64_t *ptrs = nullptr, *d_ptrs = nullptr;       // pinned
+        int16_t *q = nullptr, *d_q = nullptr;
+        uint32_t *hash = nullptr, *d_hash = nullptr;
+        uint32_t *qidx = nullptr, *d_qidx = nullptr;
+        uint32_t *qstart = nullptr, *d_qstart = nullptr;
+        uint64_t *next = nullptr, *d_next = nullptr;       // host-coherent
+        uint32_t *stop = nullptr, *d_stop = nullptr;       // host-coherent
+        uint8_t *win = nullptr;                            // device scratch
+        uint16_t *len = nullptr;
+        uint64_t issued = 0;       // last ticket handed out
+        struct Out {
+            int16_t *q;
+            uint32_t *hash, *qidx, *qstart;
+            uint32_t n;
+            bool collected;
+        } *out = nullptr;          // [nslots]
+    } w;
     // The compaction workspace is shared by every dispatch of the context; a
     // dispatch on a different stream than the previous one first waits for
     // the work queued on that stream (recorded at the switch, so same-stream
@@ -1837,6 +2056,9 @@ void host_reg_release(void *base)
         g_reg.erase(it);
     }
 }
+
+int worker_halt(yrss_ctx *c);
+void worker_free(yrss_ctx *c);
 
 // A scan look-back that never resolved leaves that batch's lists invalid.
 bool take_scan_fault(yrss_ctx *c)
@@ -2179,6 +2401,10 @@ void yrss_fini(yrss_ctx *c)
     if (!c)
         return;
     (void)hipSetDevice(c->device);
+    if (c->w.on) {
+        (void)worker_halt(c);
+        worker_free(c);
+    }
     c->pend.active = false;   // its outputs are abandoned with the context
     // device dispatches may still run on the caller's streams: drain the
     // device before the workspace goes
@@ -2459,6 +2685,9 @@ int yrss_register_host_memory(yrss_ctx *c, void *base, size_t len)
     if (!c || !base || !len || c->nranges >= YRSS_MAX_HOST_RANGES)
         return -EINVAL;
     YRSS_HIP(hipSetDevice(c->device));
+    int hrc = worker_halt(c);   // a running worker has the old range table
+    if (hrc)
+        return hrc;
     YRSS_HIP(host_reg_acquire(base, len));
     void *dev = nullptr;
     hipError_t e = hipHostGetDevicePointer(&dev, base, 0);
@@ -2481,6 +2710,9 @@ int yrss_unregister_host_memory(yrss_ctx *c, void *base)
     for (uint32_t r = 0; r < c->nranges; ++r)
         if (c->range_base[r] == base) {
             YRSS_HIP(hipSetDevice(c->device));
+            const int hrc = worker_halt(c);
+            if (hrc)
+                return hrc;
             host_reg_release(base);
             for (uint32_t k = r + 1; k < c->nranges; ++k) {
                 c->ranges[k - 1] = c->ranges[k];
@@ -2858,6 +3090,233 @@ int yrss_synth_dev(yrss_ctx *c, const struct yrss_synth_params *p, uint64_t firs
                        *p, first, n, d_win, win_stride, d_len);
     YRSS_HIP(hipGetLastError());
     return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+void worker_free(yrss_ctx *c)
+{
+    auto &w = c->w;
+    (void)hipHostFree(w.slots);
+    (void)hipHostFree(w.ptrs);
+    (void)hipHostFree(w.q);
+    (void)hipHostFree(w.hash);
+    (void)hipHostFree(w.qidx);
+    (void)hipHostFree(w.qstart);
+    (void)hipHostFree(w.next);
+    (void)hipHostFree(w.stop);
+    (void)hipFree(w.win);
+    (void)hipFree(w.len);
+    if (w.stream)
+        (void)hipStreamDestroy(w.stream);
+    delete[] w.out;
+    w = yrss_ctx::WorkerState{};
+}
+
+// Ask a running worker launch to leave and wait for it.  Every workgroup
+// polls the stop word between bursts; tickets already published stay in the
+// ring and are served by the next launch.
+int worker_halt(yrss_ctx *c)
+{
+    auto &w = c->w;
+    if (!w.running)
+        return 0;
+    __atomic_store_n(w.stop, 1u, __ATOMIC_RELEASE);
+    const hipError_t e = hipStreamSynchronize(w.stream);
+    __atomic_store_n(w.stop, 0u, __ATOMIC_RELEASE);
+    w.running = false;
+    return e == hipSuccess ? 0 : hip_fail("worker halt", e);
+}
+
+int worker_launch(yrss_ctx *c)
+{
+    auto &w = c->w;
+    WorkerParams W;
+    memset(&W, 0, sizeof(W));
+    W.P = c->proto;
+    W.P.kni_bm = c->d_kni;
+    W.P.kni_enable = 0;
+    const yrss_mbuf_layout &ml = c->cfg.mbuf;
+    W.G.nranges = c->nranges;
+    W.G.off_buf_addr = ml.off_buf_addr;
+    W.G.off_data_off = ml.off_data_off;
+    W.G.off_data_len = ml.off_data_len;
+    W.G.off_hash_rss = ml.off_hash_rss;
+    memcpy(W.G.ranges, c->ranges, sizeof(W.G.ranges));
+    W.slots = w.d_slots;
+    W.ptrs = w.d_ptrs;
+    W.q = w.d_q;
+    W.hash = w.d_hash;
+    W.qidx = w.d_qidx;
+    W.qstart = w.d_qstart;
+    W.win = w.win;
+    W.len = w.len;
+    W.next = w.d_next;
+    W.stop = w.d_stop;
+    W.nslots = w.nslots;
+    W.qs_stride = w.qs_stride;
+    W.idle_ticks = w.idle_ticks;
+    W.life_ticks = w.life_ticks;
+    hipLaunchKernelGGL(yrss_burst_worker, dim3(w.nblocks), dim3(kSmallBlock),
+                       worker_lds(c->nb), w.stream, W);
+    YRSS_HIP(hipGetLastError());
+    w.running = true;
+    return 0;
+}
+
+// The launch left (idle or lifetime cap) while tickets may be pending: start
+// another one, which resumes every workgroup at its next ticket.
+int worker_ensure(yrss_ctx *c)
+{
+    auto &w = c->w;
+    if (w.running && hipStreamQuery(w.stream) == hipSuccess)
+        w.running = false;
+    return w.running ? 0 : worker_launch(c);
+}
+
+}  // namespace
+
+extern "C" {
+
+int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
+{
+    if (!c || nblocks < 1 || nblocks > YRSS_WORKER_MAX_BLOCKS || nslots < nblocks ||
+        nslots > YRSS_WORKER_MAX_SLOTS || nslots % nblocks || c->nb > kSmallMaxNb)
+        return -EINVAL;
+    if (c->w.on)
+        return -EBUSY;
+    YRSS_HIP(hipSetDevice(c->device));
+    auto &w = c->w;
+    w.nslots = nslots;
+    w.nblocks = nblocks;
+    w.qs_stride = (c->nb + 1u + 15u) & ~15u;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess ||
+        khz <= 0)
+        khz = 100000;   // s_memrealtime runs at 100 MHz on CDNA
+    const char *ei = getenv("YRSS_WORKER_IDLE_MS");
+    const char *el = getenv("YRSS_WORKER_LIFE_MS");
+    const uint64_t idle_ms = ei ? strtoull(ei, nullptr, 10) : 50u;
+    const uint64_t life_ms = el ? strtoull(el, nullptr, 10) : 1000u;
+    w.idle_ticks = std::min<uint64_t>(idle_ms, 10000u) * (uint64_t)khz;
+    w.life_ticks = std::min<uint64_t>(std::max<uint64_t>(life_ms, 1u), 10000u) * (uint64_t)khz;
+    const size_t S = nslots, M = kWorkerMaxBurst;
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&w.slots, S * sizeof(WorkerSlot), hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipHostMalloc((void **)&w.next, nblocks * sizeof(uint64_t), hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipHostMalloc((void **)&w.stop, sizeof(uint32_t), hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipHostMalloc((void **)&w.ptrs, S * M * 8u, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&w.q, S * M * 2u, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&w.hash, S * M * 4u, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&w.qidx, S * M * 4u, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&w.qstart, S * w.qs_stride * 4u, hipHostMallocDefault)) !=
+            hipSuccess ||
+        (e = hipMalloc((void **)&w.win, (size_t)nblocks * M * YRSS_WIN_FULL)) != hipSuccess ||
+        (e = hipMalloc((void **)&w.len, (size_t)nblocks * M * 2u)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_slots, w.slots, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_next, w.next, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_stop, w.stop, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_ptrs, w.ptrs, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_q, w.q, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_hash, w.hash, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_qidx, w.qidx, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_qstart, w.qstart, 0)) != hipSuccess) {
+        worker_free(c);
+        return hip_fail("yrss_worker_start", e);
+    }
+    memset((void *)w.slots, 0, S * sizeof(WorkerSlot));
+    for (uint32_t b = 0; b < nblocks; ++b)
+        w.next[b] = b + 1u;            // tickets start at 1; block b serves b+1, b+1+B, ...
+    *w.stop = 0;
+    w.out = new yrss_ctx::WorkerState::Out[S];
+    for (size_t i = 0; i < S; ++i)
+        w.out[i] = yrss_ctx::WorkerState::Out{nullptr, nullptr, nullptr, nullptr, 0u, true};
+    w.issued = 0;
+    w.on = true;
+    return 0;
+}
+
+int yrss_worker_submit(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out_q,
+                       uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                       uint32_t flags, uint64_t *ticket)
+{
+    if (!c || !ticket || (n && (!mbufs || !out_q)) || (flags & ~YRSS_F_WRITE_RSS))
+        return -EINVAL;
+    auto &w = c->w;
+    if (!w.on)
+        return -ENODEV;
+    if (n > kWorkerMaxBurst)
+        return -E2BIG;
+    const uint64_t t = w.issued + 1u;
+    const uint32_t si = (uint32_t)(t % w.nslots);
+    if (!w.out[si].collected)
+        return -EBUSY;   // the slot's previous ticket was not polled yet
+    YRSS_HIP(hipSetDevice(c->device));
+    WorkerSlot *sl = w.slots + si;
+    memcpy(w.ptrs + (size_t)si * kWorkerMaxBurst, mbufs, (size_t)n * 8u);
+    sl->n = n;
+    sl->flags = flags;
+    w.out[si] = yrss_ctx::WorkerState::Out{out_q, out_hash, out_qidx, out_qstart, n, false};
+    __atomic_store_n(&sl->seq, t, __ATOMIC_RELEASE);
+    w.issued = t;
+    *ticket = t;
+    return worker_ensure(c);
+}
+
+int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
+{
+    if (!c || !c->w.on || ticket == 0 || ticket > c->w.issued)
+        return -EINVAL;
+    auto &w = c->w;
+    const uint32_t si = (uint32_t)(ticket % w.nslots);
+    WorkerSlot *sl = w.slots + si;
+    auto &o = w.out[si];
+    if (ticket + w.nslots <= w.issued || o.collected)
+        return -EINVAL;   // reused or already collected
+    uint64_t spins = 0;
+    while (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != ticket) {
+        if ((++spins & 1023u) == 0) {
+            YRSS_HIP(hipSetDevice(c->device));
+            int rc = worker_ensure(c);   // the launch may have left while idle
+            if (rc)
+                return rc;
+        }
+        if (!wait)
+            return -EAGAIN;
+        if (spins > (1ull << 32))
+            return -ETIMEDOUT;
+        __builtin_ia32_pause();
+    }
+    o.collected = true;
+    if (__atomic_load_n(&sl->fault, __ATOMIC_ACQUIRE))
+        return -EFAULT;
+    const size_t base = (size_t)si * kWorkerMaxBurst;
+    memcpy(o.q, w.q + base, (size_t)o.n * 2u);
+    if (o.hash)
+        memcpy(o.hash, w.hash + base, (size_t)o.n * 4u);
+    if (o.qidx)
+        memcpy(o.qidx, w.qidx + base, (size_t)o.n * 4u);
+    if (o.qstart)
+        memcpy(o.qstart, w.qstart + (size_t)si * w.qs_stride, (c->nb + 1u) * 4u);
+    return 0;
+}
+
+int yrss_worker_stop(yrss_ctx *c)
+{
+    if (!c)
+        return -EINVAL;
+    if (!c->w.on)
+        return 0;
+    YRSS_HIP(hipSetDevice(c->device));
+    const int rc = worker_halt(c);
+    worker_free(c);
+    return rc;
 }
 
 int yrss_status(yrss_ctx *c)

@@ -214,6 +214,44 @@ class SoftRss:
         self._inflight = None
         abi.check(rc, "yrss_wait")
 
+    # -- persistent burst worker ------------------------------------------------
+    def worker_start(self, nslots: int = 16, nblocks: int = 4) -> None:
+        """Start the persistent small-burst worker (``yrss_worker_start``)."""
+        abi.check(self._lib.yrss_worker_start(self._ctx, nslots, nblocks), "yrss_worker_start")
+        self._wk = {}
+
+    def worker_submit(self, mbuf_ptrs: np.ndarray, want_hash=True, compact=True,
+                      write_rss=False) -> int:
+        """Queue one burst of ``struct rte_mbuf *`` (registered memory); returns
+        its ticket.  :meth:`worker_poll` returns the DispatchResult."""
+        mb = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
+        n = int(mb.size)
+        q = np.empty(max(n, 1), np.int16)
+        h = np.empty(max(n, 1), np.uint32) if want_hash else None
+        qi = np.empty(max(n, 1), np.uint32) if compact else None
+        qs = np.empty(self.nb_queues + 2, np.uint32) if compact else None
+        t = ctypes.c_uint64()
+        rc = self._lib.yrss_worker_submit(self._ctx, _ptr(mb), n, _ptr(q), _ptr(h), _ptr(qi),
+                                          _ptr(qs), abi.F_WRITE_RSS if write_rss else 0,
+                                          ctypes.byref(t))
+        abi.check(rc, "yrss_worker_submit")
+        self._wk[t.value] = DispatchResult(q[:n], None if h is None else h[:n],
+                                           None if qi is None else qi[:n], qs)
+        return t.value
+
+    def worker_poll(self, ticket: int, wait: bool = True):
+        """The burst's DispatchResult, or None while it is pending (wait=False)."""
+        rc = self._lib.yrss_worker_poll(self._ctx, ticket, 1 if wait else 0)
+        if rc == -11:   # -EAGAIN
+            return None
+        res = self._wk.pop(ticket, None)
+        abi.check(rc, "yrss_worker_poll")
+        return res
+
+    def worker_stop(self) -> None:
+        abi.check(self._lib.yrss_worker_stop(self._ctx), "yrss_worker_stop")
+        self._wk = {}
+
     def register_host_memory(self, base: int, nbytes: int) -> None:
         abi.check(self._lib.yrss_register_host_memory(self._ctx, base, nbytes),
                   "yrss_register_host_memory")
