@@ -225,6 +225,22 @@ def pcie_inclusive(profile: str):
                 continue
             out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
                         "mpps": d["mpps"], "note": d.get("note", "")})
+    # persistent worker: 32 workgroups, 128 bursts in flight, bursts of 32 and 1024
+    try:
+        r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), "0", "1"],
+                           capture_output=True, text=True, timeout=240,
+                           env={**os.environ, "YRSS_CBENCH_MODES": "4",
+                                "YRSS_CBENCH_WORKER_DEPTH": "128",
+                                "YRSS_CBENCH_WORKER_BLOCKS": "32"})
+        for line in r.stdout.splitlines():
+            try:
+                d = json.loads(line)
+            except ValueError:
+                continue
+            out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
+                        "blocks": d.get("blocks"), "mpps": d["mpps"], "note": d.get("note", "")})
+    except subprocess.TimeoutExpired:
+        pass
     return out or None
 
 
