@@ -384,7 +384,7 @@ int yrss_timing_read(yrss_ctx *ctx, int kernel, double *total_ms,
  * unregistering host memory restarts it.  nslots is a multiple of nblocks;
  * nb_queues + 1 <= 64. */
 #define YRSS_WORKER_MAX_BURST 1024
-#define YRSS_WORKER_MAX_BLOCKS 32
+#define YRSS_WORKER_MAX_BLOCKS 128
 #define YRSS_WORKER_MAX_SLOTS 4096
 int yrss_worker_start(yrss_ctx *ctx, uint32_t nslots, uint32_t nblocks);
 /* Queue one burst (n <= YRSS_WORKER_MAX_BURST; flags: YRSS_F_WRITE_RSS);
@@ -393,6 +393,12 @@ int yrss_worker_start(yrss_ctx *ctx, uint32_t nslots, uint32_t nblocks);
 int yrss_worker_submit(yrss_ctx *ctx, void *const *mbufs, uint32_t n, int16_t *out_q,
                        uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
                        uint32_t flags, uint64_t *ticket);
+/* Same for (data pointer, data_len) pairs the host already holds, like
+ * yrss_dispatch_frames_zc: the GPU reads only the windows (in registered
+ * memory). */
+int yrss_worker_submit_frames(yrss_ctx *ctx, const uint8_t *const *data, const uint16_t *len,
+                              uint32_t n, int16_t *out_q, uint32_t *out_hash,
+                              uint32_t *out_qidx, uint32_t *out_qstart, uint64_t *ticket);
 /* 0: the burst is done and its outputs copied; -EAGAIN: not yet (wait = 0);
  * -EFAULT: a mbuf or its data lies outside every registered range. */
 int yrss_worker_poll(yrss_ctx *ctx, uint64_t ticket, int wait);

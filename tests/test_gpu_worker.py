@@ -2,6 +2,7 @@
 to a resident gfx950 kernel through a ring in host-coherent memory, checked
 against the oracle; relaunch after an idle exit; fault and limit reporting.
 """
+import ctypes
 import time
 
 import numpy as np
@@ -113,5 +114,41 @@ def test_worker_errors(dev, oracle_mod):
             eng.worker_poll(tb)                                       # -EFAULT
         q, h, qi, qs = _expect(oracle_mod, frames[:20], cfg)
         _check(eng.worker_poll(t2), q, h, qi, qs)
+        eng.worker_stop()
+        eng.unregister_host_memory(pool.ctypes.data)
+
+
+def test_worker_frames(dev, oracle_mod):
+    """yrss_worker_submit_frames: (data, data_len) pairs; the GPU reads only
+    the windows."""
+    cfg = (8, 8, 1, 0)
+    sizes = [32, 1, 1024, 500, 0, 77]
+    frames = _frames(oracle_mod, sum(sizes), 55)
+    pool, ptrs, _ = _fake_mbufs(frames, headroom=130)
+    data = (ptrs + np.uint64(128 + 130)).astype(np.uint64)
+    flen = np.array([len(f) for f in frames], np.uint16)
+    q_all, h_all, _, _ = _expect(oracle_mod, frames, cfg)
+    lib = abi.load()
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(8, 2)
+        off = 0
+        for n in sizes:
+            q = np.empty(max(n, 1), np.int16)
+            h = np.empty(max(n, 1), np.uint32)
+            qi = np.empty(max(n, 1), np.uint32)
+            qs = np.empty(cfg[1] + 2, np.uint32)
+            t = ctypes.c_uint64()
+            rc = lib.yrss_worker_submit_frames(eng._ctx, data[off:].ctypes.data,
+                                               flen[off:].ctypes.data, n, q.ctypes.data,
+                                               h.ctypes.data, qi.ctypes.data, qs.ctypes.data,
+                                               ctypes.byref(t))
+            assert rc == 0
+            assert lib.yrss_worker_poll(eng._ctx, t.value, 1) == 0
+            qr = q_all[off:off + n]
+            qi_ref, qs_ref = oracle_mod.process_burst(qr, cfg[1])
+            assert np.array_equal(q[:n], qr) and np.array_equal(h[:n], h_all[off:off + n])
+            assert np.array_equal(qi[:n], qi_ref) and np.array_equal(qs[: qs_ref.size], qs_ref)
+            off += n
         eng.worker_stop()
         eng.unregister_host_memory(pool.ctypes.data)

@@ -54,8 +54,12 @@ static double now(void)
 static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_sz,
                       uint8_t *arena, size_t arena_sz, void **mbufs, uint32_t pool, uint32_t B,
                       double secs, int16_t *q_all, uint32_t *h_all, uint32_t *qi_all,
-                      uint32_t profile, int thp)
+                      uint32_t profile, int thp, const uint8_t **fdata, uint16_t *flen)
 {
+    const char *fe = getenv("YRSS_CBENCH_WORKER_FRAMES");
+    const int frames = fe && atoi(fe) != 0;
+    if (frames)
+        fill_frames(mbufs, pool, fdata, flen);   /* outside the timed region */
     const char *de = getenv("YRSS_CBENCH_WORKER_DEPTH");
     const char *be = getenv("YRSS_CBENCH_WORKER_BLOCKS");
     unsigned blocks = be ? (unsigned)atoi(be) : 4u;
@@ -95,8 +99,11 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
                 fprintf(stderr, "worker poll: %d\n", rc);
                 return 3;
             }
-            if ((rc = yrss_worker_submit(ctx, mbufs + off, B, q_all + off, h_all + off,
-                                         qi_all + off, qs[k], 0, &tk[k])) != 0) {
+            rc = frames ? yrss_worker_submit_frames(ctx, fdata + off, flen + off, B, q_all + off,
+                                                    h_all + off, qi_all + off, qs[k], &tk[k])
+                        : yrss_worker_submit(ctx, mbufs + off, B, q_all + off, h_all + off,
+                                             qi_all + off, qs[k], 0, &tk[k]);
+            if (rc != 0) {
                 fprintf(stderr, "worker submit: %d\n", rc);
                 return 3;
             }
@@ -112,12 +119,13 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
             return 3;
         }
     t1 = now();
-    printf("{\"tool\": \"yrss_cbench\", \"api\": \"yrss_worker\", \"profile\": %u, "
+    printf("{\"tool\": \"yrss_cbench\", \"api\": \"%s\", \"profile\": %u, "
            "\"burst\": %u, \"inflight\": %u, \"blocks\": %u, \"pkts\": %llu, "
            "\"seconds\": %.3f, \"mpps\": %.2f, \"us_per_burst\": %.2f, \"thp\": %d, "
            "\"mode\": 4, \"note\": \"persistent kernel polls a ring of bursts in pinned "
            "memory; mbufs read over PCIe\"}\n",
-           profile, B, depth, blocks, (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
+           frames ? "yrss_worker_submit_frames" : "yrss_worker_submit", profile, B, depth,
+           blocks, (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
            (t1 - t0) / (pkts / (double)B) * 1e6, thp);
     fflush(stdout);
     free(tk);
@@ -292,7 +300,7 @@ int main(int argc, char **argv)
         for (unsigned bi = 0; bi < 2; ++bi) {
             const uint32_t B = burst_arg ? burst_arg : bursts[bi];
             const int rc = run_worker(&cfg, mem, mem_sz, arena, arena_sz, mbufs, pool, B, secs,
-                                      q_all, h_all, qi_all, profile, thp);
+                                      q_all, h_all, qi_all, profile, thp, fdata, flen);
             if (rc)
                 return rc;
             if (burst_arg)

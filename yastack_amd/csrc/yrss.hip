@@ -1170,11 +1170,12 @@ struct GatherIO {
     uint16_t *len;
     uint32_t *fault;
     uint32_t n;
+    uint32_t frames;     // 1: ptrs are frame data pointers, lens given
 };
 
 __device__ __forceinline__ GatherIO gather_io(const GatherParams &G)
 {
-    return GatherIO{G.ptrs, G.lens, G.win, G.len, G.fault, G.n};
+    return GatherIO{G.ptrs, G.lens, G.win, G.len, G.fault, G.n, G.frames};
 }
 
 template <int kB>
@@ -1190,9 +1191,9 @@ __device__ __forceinline__ void gather_quads(const GatherParams &G, const Gather
         for (int k = 0; k < kB; ++k) {
             idx[k] = p0 + 16u * k + (lane >> 2);
             m[k] = idx[k] < io.n ? io.ptrs[idx[k]] : 0u;
-            L[k] = (G.frames && idx[k] < io.n) ? io.lens[idx[k]] : 0u;
+            L[k] = (io.frames && idx[k] < io.n) ? io.lens[idx[k]] : 0u;
         }
-        if (G.frames) {
+        if (io.frames) {
             // frames mode: the host already knows data pointer and data_len
 #pragma unroll
             for (int k = 0; k < kB; ++k) {
@@ -1486,19 +1487,21 @@ constexpr uint32_t kWorkerMaxBurst = YRSS_WORKER_MAX_BURST;   // 16 tiles: one p
 
 struct alignas(64) WorkerSlot {
     uint64_t seq;        // host: ticket, written last (release)
+    uint32_t n;          // host: packets (written before seq; read with it, one 16-B load)
+    uint32_t flags;      // host: YRSS_F_WRITE_RSS | kWorkerFrames
     uint64_t done;       // GPU: ticket, written after the outputs (release, system)
-    uint32_t n;
-    uint32_t flags;      // YRSS_F_WRITE_RSS
     uint32_t fault;      // GPU: a pointer outside every registered range
     uint32_t pad_[9];
 };
+constexpr uint32_t kWorkerFrames = 1u << 16;   // slot holds (data, data_len) pairs
 static_assert(sizeof(WorkerSlot) == 64, "one line per slot header");
 
 struct WorkerParams {
     ParseParams P;       // configuration (per-burst fields set in the kernel)
     GatherParams G;      // range table and mbuf layout
     WorkerSlot *slots;   // [nslots] host-coherent
-    uint64_t *ptrs;      // [nslots][kWorkerMaxBurst] pinned
+    uint64_t *ptrs;      // [nslots][kWorkerMaxBurst] pinned: mbuf or frame data pointers
+    uint16_t *lens;      // [nslots][kWorkerMaxBurst] pinned: frame data_len (frames mode)
     int16_t *q;          // [nslots][kWorkerMaxBurst] pinned outputs
     uint32_t *hash;
     uint32_t *qidx;
@@ -1534,8 +1537,12 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         if (threadIdx.x == 0) {
             uint32_t go = 0;   // 1: a burst, 2: leave
             for (;;) {
-                if (__hip_atomic_load(&sl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ==
-                    t) {
+                // seq, n and flags in one 16-byte read: the host writes n and
+                // flags before seq, so a new seq comes with its n and flags
+                const u32x4 hd = *reinterpret_cast<const volatile u32x4 *>(sl);
+                if ((((uint64_t)hd.y << 32) | hd.x) == t) {
+                    ctl[1] = hd.z;
+                    ctl[2] = hd.w;
                     go = 1;
                     break;
                 }
@@ -1549,9 +1556,6 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
             }
             if (go == 1) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                ctl[1] = __hip_atomic_load(&sl->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                ctl[2] = __hip_atomic_load(&sl->flags, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&sl->fault, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             ctl[0] = go;
@@ -1571,14 +1575,15 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         P.rank = nullptr;
         P.seg_cnt = nullptr;
         P.out16 = 0;
-        const GatherIO gio{W.ptrs + (size_t)si * kWorkerMaxBurst, nullptr,
-                           const_cast<uint8_t *>(P.win), const_cast<uint16_t *>(P.len),
-                           &sl->fault, n};
+        const uint32_t frames = (ctl[2] & kWorkerFrames) ? 1u : 0u;
+        const GatherIO gio{W.ptrs + (size_t)si * kWorkerMaxBurst,
+                           W.lens + (size_t)si * kWorkerMaxBurst, const_cast<uint8_t *>(P.win),
+                           const_cast<uint16_t *>(P.len), &sl->fault, n, frames};
         if (n) {
             small_burst_body<false, 1>(P, W.G, gio,
                                     BurstIO{W.qidx + (size_t)si * kWorkerMaxBurst,
                                             W.qstart + (size_t)si * W.qs_stride, 1u,
-                                            (ctl[2] & YRSS_F_WRITE_RSS) ? 1u : 0u},
+                                            (!frames && (ctl[2] & YRSS_F_WRITE_RSS)) ? 1u : 0u},
                                     L, wave, lane);
         } else if (threadIdx.x <= W.P.nb) {
             W.qstart[(size_t)si * W.qs_stride + threadIdx.x] = 0u;
@@ -1744,6 +1749,7 @@ struct yrss_ctx {
         hipStream_t stream = nullptr;
         WorkerSlot *slots = nullptr, *d_slots = nullptr;   // host-coherent
         uint64_t *ptrs = nullptr, *d_ptrs = nullptr;       // pinned
+        uint16_t *lens = nullptr, *d_lens = nullptr;       // pinned (frames mode)
         int16_t *q = nullptr, *d_q = nullptr;
         uint32_t *hash = nullptr, *d_hash = nullptr;
         uint32_t *qidx = nullptr, *d_qidx = nullptr;
@@ -3101,6 +3107,7 @@ void worker_free(yrss_ctx *c)
     auto &w = c->w;
     (void)hipHostFree(w.slots);
     (void)hipHostFree(w.ptrs);
+    (void)hipHostFree(w.lens);
     (void)hipHostFree(w.q);
     (void)hipHostFree(w.hash);
     (void)hipHostFree(w.qidx);
@@ -3147,6 +3154,7 @@ int worker_launch(yrss_ctx *c)
     memcpy(W.G.ranges, c->ranges, sizeof(W.G.ranges));
     W.slots = w.d_slots;
     W.ptrs = w.d_ptrs;
+    W.lens = w.d_lens;
     W.q = w.d_q;
     W.hash = w.d_hash;
     W.qidx = w.d_qidx;
@@ -3212,6 +3220,7 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
         (e = hipHostMalloc((void **)&w.stop, sizeof(uint32_t), hipHostMallocCoherent)) !=
             hipSuccess ||
         (e = hipHostMalloc((void **)&w.ptrs, S * M * 8u, hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&w.lens, S * M * 2u, hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void **)&w.q, S * M * 2u, hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void **)&w.hash, S * M * 4u, hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void **)&w.qidx, S * M * 4u, hipHostMallocDefault)) != hipSuccess ||
@@ -3223,6 +3232,7 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
         (e = hipHostGetDevicePointer((void **)&w.d_next, w.next, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_stop, w.stop, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_ptrs, w.ptrs, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_lens, w.lens, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_q, w.q, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_hash, w.hash, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_qidx, w.qidx, 0)) != hipSuccess ||
@@ -3242,12 +3252,14 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
     return 0;
 }
 
-int yrss_worker_submit(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out_q,
-                       uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
-                       uint32_t flags, uint64_t *ticket)
+}  // extern "C"
+
+namespace {
+
+int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
+                  int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                  uint32_t flags, uint64_t *ticket)
 {
-    if (!c || !ticket || (n && (!mbufs || !out_q)) || (flags & ~YRSS_F_WRITE_RSS))
-        return -EINVAL;
     auto &w = c->w;
     if (!w.on)
         return -ENODEV;
@@ -3259,14 +3271,42 @@ int yrss_worker_submit(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out
         return -EBUSY;   // the slot's previous ticket was not polled yet
     YRSS_HIP(hipSetDevice(c->device));
     WorkerSlot *sl = w.slots + si;
-    memcpy(w.ptrs + (size_t)si * kWorkerMaxBurst, mbufs, (size_t)n * 8u);
+    memcpy(w.ptrs + (size_t)si * kWorkerMaxBurst, ptrs, (size_t)n * 8u);
+    if (lens)
+        memcpy(w.lens + (size_t)si * kWorkerMaxBurst, lens, (size_t)n * 2u);
     sl->n = n;
     sl->flags = flags;
     w.out[si] = yrss_ctx::WorkerState::Out{out_q, out_hash, out_qidx, out_qstart, n, false};
-    __atomic_store_n(&sl->seq, t, __ATOMIC_RELEASE);
+    __atomic_store_n(&sl->seq, t, __ATOMIC_RELEASE);   // n and flags become visible first
     w.issued = t;
     *ticket = t;
-    return worker_ensure(c);
+    // no stream query per burst (it costs more than the rest of a submit): a
+    // launch that left while idle is noticed and relaunched by the poll
+    return w.running ? 0 : worker_launch(c);
+}
+
+}  // namespace
+
+extern "C" {
+
+int yrss_worker_submit(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out_q,
+                       uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                       uint32_t flags, uint64_t *ticket)
+{
+    if (!c || !ticket || (n && (!mbufs || !out_q)) || (flags & ~YRSS_F_WRITE_RSS))
+        return -EINVAL;
+    return worker_submit(c, mbufs, nullptr, n, out_q, out_hash, out_qidx, out_qstart, flags,
+                         ticket);
+}
+
+int yrss_worker_submit_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t *len,
+                              uint32_t n, int16_t *out_q, uint32_t *out_hash,
+                              uint32_t *out_qidx, uint32_t *out_qstart, uint64_t *ticket)
+{
+    if (!c || !ticket || (n && (!data || !len || !out_q)))
+        return -EINVAL;
+    return worker_submit(c, data, len, n, out_q, out_hash, out_qidx, out_qstart, kWorkerFrames,
+                         ticket);
 }
 
 int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
@@ -3281,7 +3321,7 @@ int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
         return -EINVAL;   // reused or already collected
     uint64_t spins = 0;
     while (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != ticket) {
-        if ((++spins & 1023u) == 0) {
+        if ((++spins & 63u) == 0) {
             YRSS_HIP(hipSetDevice(c->device));
             int rc = worker_ensure(c);   // the launch may have left while idle
             if (rc)
