@@ -379,10 +379,11 @@ int yrss_timing_read(yrss_ctx *ctx, int kernel, double *total_ms,
  * slot; poll copies them to the caller's arrays.  Up to nslots bursts are in
  * flight; every ticket must be polled before its slot is reused (submit
  * returns -EBUSY otherwise).  The kernel leaves after YRSS_WORKER_IDLE_MS
- * (default 50) without work or YRSS_WORKER_LIFE_MS (default 1000) in total and
- * is relaunched transparently by the next submit or poll; registering or
- * unregistering host memory restarts it.  nslots is a multiple of nblocks;
- * nb_queues + 1 <= 64. */
+ * (default 50) without a submit or YRSS_WORKER_LIFE_MS (default 1000) in total
+ * and is relaunched transparently by the next submit or poll (also by a
+ * wait = 0 poll); registering or unregistering host memory restarts it.
+ * nslots is a multiple of nblocks; nb_queues + 1 <= 64.  Submits and polls of
+ * one context come from one thread at a time (the dispatcher lcore). */
 #define YRSS_WORKER_MAX_BURST 1024
 #define YRSS_WORKER_MAX_BLOCKS 128
 #define YRSS_WORKER_MAX_SLOTS 4096

@@ -99,7 +99,7 @@ def test_worker_errors(dev, oracle_mod):
     lib = abi.load()
     with SoftRss(*cfg, device=0, max_burst=0) as eng:
         assert lib.yrss_worker_start(eng._ctx, 6, 4) == -22          # nslots % nblocks
-        assert lib.yrss_worker_start(eng._ctx, 4, 64) == -22         # too many blocks
+        assert lib.yrss_worker_start(eng._ctx, 256, 256) == -22       # too many blocks
         eng.register_host_memory(pool.ctypes.data, pool.nbytes)
         eng.worker_start(2, 1)
         with pytest.raises(abi.YrssError):
@@ -150,5 +150,57 @@ def test_worker_frames(dev, oracle_mod):
             assert np.array_equal(q[:n], qr) and np.array_equal(h[:n], h_all[off:off + n])
             assert np.array_equal(qi[:n], qi_ref) and np.array_equal(qs[: qs_ref.size], qs_ref)
             off += n
+        eng.worker_stop()
+        eng.unregister_host_memory(pool.ctypes.data)
+
+
+def test_worker_low_rate_no_stall(dev, oracle_mod, monkeypatch):
+    """Fewer than B bursts per idle period: idle is judged over the whole
+    ring, so no workgroup leaves while the others keep serving (its tickets
+    would wait for the rest of the launch to go idle)."""
+    monkeypatch.setenv("YRSS_WORKER_IDLE_MS", "5")
+    cfg = (4, 4, 1, 1)
+    nb, per, nburst = 8, 16, 40
+    frames = _frames(oracle_mod, per * nburst, 77)
+    pool, ptrs, _ = _fake_mbufs(frames)
+    q, h, _, _ = _expect(oracle_mod, frames, cfg)
+    lat = []
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(nb, nb)
+        for k in range(nburst):
+            lo = per * k
+            t = eng.worker_submit(ptrs[lo:lo + per])
+            t0 = time.perf_counter()
+            r = eng.worker_poll(t)
+            lat.append(time.perf_counter() - t0)
+            qi, qs = oracle_mod.process_burst(q[lo:lo + per], cfg[1])
+            _check(r, q[lo:lo + per], h[lo:lo + per], qi, qs)
+            time.sleep(0.002)        # each workgroup sees a burst every ~16 ms
+        eng.worker_stop()
+        eng.unregister_host_memory(pool.ctypes.data)
+    # the first burst includes the launch; a stranded ticket would take >= 5 ms
+    assert max(lat[1:]) < 0.003, sorted(lat)[-5:]
+
+
+def test_worker_relaunch_nonblocking_poll(dev, oracle_mod, monkeypatch):
+    """After the launch left, a poller that never blocks (wait=0) still gets
+    the burst served: the poll relaunches."""
+    monkeypatch.setenv("YRSS_WORKER_IDLE_MS", "2")
+    cfg = (3, 3, 1, 1)
+    frames = _frames(oracle_mod, 64, 78)
+    pool, ptrs, _ = _fake_mbufs(frames)
+    q, h, qi, qs = _expect(oracle_mod, frames[:32], cfg)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(4, 4)
+        for _ in range(3):
+            t = eng.worker_submit(ptrs[:32])
+            r, deadline = None, time.time() + 5.0
+            while r is None and time.time() < deadline:
+                r = eng.worker_poll(t, wait=False)
+            assert r is not None
+            _check(r, q, h, qi, qs)
+            time.sleep(0.02)         # past the idle limit: every workgroup leaves
         eng.worker_stop()
         eng.unregister_host_memory(pool.ctypes.data)

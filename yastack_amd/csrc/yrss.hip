@@ -1476,8 +1476,10 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
 // small_burst_body() (tables stay in LDS across bursts), writes q / hash /
 // lists into the slot's pinned output area and publishes the ticket in the
 // slot's done word.  Every workgroup leaves when the host sets the stop word,
-// after idle_ticks without work, or after life_ticks in total, storing the
-// ticket it would have served next; the host relaunches on the next submit.
+// after the whole ring saw no submit for idle_ticks, or after life_ticks in
+// total, storing the ticket it would have served next and counting itself in
+// WorkerCtl::exited; the host's next submit or poll then stops the rest of
+// the launch and relaunches.
 // Protocol (host-coherent memory, system scope): the host writes ptrs / n /
 // flags, then seq with release; the GPU polls seq relaxed, then acquires.
 // The GPU drains every wave's output stores (vmcnt(0) + barrier), releases
@@ -1496,6 +1498,18 @@ struct alignas(64) WorkerSlot {
 constexpr uint32_t kWorkerFrames = 1u << 16;   // slot holds (data, data_len) pairs
 static_assert(sizeof(WorkerSlot) == 64, "one line per slot header");
 
+// Launch control, host-coherent.  Line 0 is written by the host only (so
+// the host's per-submit store stays a cache hit), line 1 by the GPU only.
+struct alignas(64) WorkerCtl {
+    uint32_t stop;       // host: leave now
+    uint32_t pad0_;
+    uint64_t pub;        // host: latest published ticket (ring activity)
+    uint32_t pad1_[12];
+    uint32_t exited;     // GPU: workgroups of this launch that left
+    uint32_t pad2_[15];
+};
+static_assert(sizeof(WorkerCtl) == 128, "two lines");
+
 struct WorkerParams {
     ParseParams P;       // configuration (per-burst fields set in the kernel)
     GatherParams G;      // range table and mbuf layout
@@ -1509,7 +1523,7 @@ struct WorkerParams {
     uint8_t *win;        // device scratch [nblocks][kWorkerMaxBurst * 80]
     uint16_t *len;       // device scratch [nblocks][kWorkerMaxBurst]
     uint64_t *next;      // host-coherent [nblocks]: ticket to serve next (resume)
-    uint32_t *stop;      // host-coherent stop word
+    WorkerCtl *wctl;     // host-coherent launch control
     uint32_t nslots;
     uint32_t qs_stride;
     uint64_t idle_ticks; // s_memrealtime ticks (100 MHz)
@@ -1531,6 +1545,9 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
                                    __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t t_begin = wall_clock64();
     uint64_t t_last = t_begin;
+    uint64_t pub_seen = 0;   // thread 0 only: ring activity at the last idle check
+    if (threadIdx.x == 0)
+        pub_seen = __hip_atomic_load(&W.wctl->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (;;) {
         const uint32_t si = (uint32_t)(t % W.nslots);
         WorkerSlot *sl = W.slots + si;
@@ -1547,10 +1564,25 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
                     break;
                 }
                 const uint64_t now = wall_clock64();
-                if (__hip_atomic_load(W.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
-                    now - t_last > W.idle_ticks || now - t_begin > W.life_ticks) {
+                if (__hip_atomic_load(&W.wctl->stop, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM) ||
+                    now - t_begin > W.life_ticks) {
                     go = 2;
                     break;
+                }
+                if (now - t_last > W.idle_ticks) {
+                    // idle is collective: leave only when the whole ring saw no
+                    // submit for an idle period, so at low rates (fewer than B
+                    // bursts per idle period) no workgroup leaves while others
+                    // keep serving and strands its tickets
+                    const uint64_t pub = __hip_atomic_load(&W.wctl->pub, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (pub == pub_seen) {
+                        go = 2;
+                        break;
+                    }
+                    pub_seen = pub;
+                    t_last = now;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
@@ -1599,8 +1631,11 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         t_last = wall_clock64();
         t += gridDim.x;
     }
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
         __hip_atomic_store(W.next + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // tells the host to retire this launch (stop the rest) and relaunch
+        __hip_atomic_fetch_add(&W.wctl->exited, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1755,7 +1790,7 @@ struct yrss_ctx {
         uint32_t *qidx = nullptr, *d_qidx = nullptr;
         uint32_t *qstart = nullptr, *d_qstart = nullptr;
         uint64_t *next = nullptr, *d_next = nullptr;       // host-coherent
-        uint32_t *stop = nullptr, *d_stop = nullptr;       // host-coherent
+        WorkerCtl *ctl = nullptr, *d_ctl = nullptr;        // host-coherent
         uint8_t *win = nullptr;                            // device scratch
         uint16_t *len = nullptr;
         uint64_t issued = 0;       // last ticket handed out
@@ -3113,7 +3148,7 @@ void worker_free(yrss_ctx *c)
     (void)hipHostFree(w.qidx);
     (void)hipHostFree(w.qstart);
     (void)hipHostFree(w.next);
-    (void)hipHostFree(w.stop);
+    (void)hipHostFree(w.ctl);
     (void)hipFree(w.win);
     (void)hipFree(w.len);
     if (w.stream)
@@ -3130,9 +3165,10 @@ int worker_halt(yrss_ctx *c)
     auto &w = c->w;
     if (!w.running)
         return 0;
-    __atomic_store_n(w.stop, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(&w.ctl->stop, 1u, __ATOMIC_RELEASE);
     const hipError_t e = hipStreamSynchronize(w.stream);
-    __atomic_store_n(w.stop, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&w.ctl->stop, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&w.ctl->exited, 0u, __ATOMIC_RELAXED);
     w.running = false;
     return e == hipSuccess ? 0 : hip_fail("worker halt", e);
 }
@@ -3162,7 +3198,7 @@ int worker_launch(yrss_ctx *c)
     W.win = w.win;
     W.len = w.len;
     W.next = w.d_next;
-    W.stop = w.d_stop;
+    W.wctl = w.d_ctl;
     W.nslots = w.nslots;
     W.qs_stride = w.qs_stride;
     W.idle_ticks = w.idle_ticks;
@@ -3174,14 +3210,19 @@ int worker_launch(yrss_ctx *c)
     return 0;
 }
 
-// The launch left (idle or lifetime cap) while tickets may be pending: start
-// another one, which resumes every workgroup at its next ticket.
+// Keep a launch resident.  A workgroup that leaves (idle ring, lifetime cap)
+// counts itself in ctl->exited, a cache hit for the host until the GPU writes
+// it: then the rest of that launch is stopped (they leave between bursts) and
+// a new one resumes every workgroup at its next ticket.  Retiring the whole
+// launch means no workgroup's tickets wait on the others' lifetime.
 int worker_ensure(yrss_ctx *c)
 {
     auto &w = c->w;
-    if (w.running && hipStreamQuery(w.stream) == hipSuccess)
-        w.running = false;
-    return w.running ? 0 : worker_launch(c);
+    if (w.running && __atomic_load_n(&w.ctl->exited, __ATOMIC_ACQUIRE) == 0u)
+        return 0;
+    YRSS_HIP(hipSetDevice(c->device));
+    const int rc = worker_halt(c);
+    return rc ? rc : worker_launch(c);
 }
 
 }  // namespace
@@ -3217,7 +3258,7 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
             hipSuccess ||
         (e = hipHostMalloc((void **)&w.next, nblocks * sizeof(uint64_t), hipHostMallocCoherent)) !=
             hipSuccess ||
-        (e = hipHostMalloc((void **)&w.stop, sizeof(uint32_t), hipHostMallocCoherent)) !=
+        (e = hipHostMalloc((void **)&w.ctl, sizeof(WorkerCtl), hipHostMallocCoherent)) !=
             hipSuccess ||
         (e = hipHostMalloc((void **)&w.ptrs, S * M * 8u, hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc((void **)&w.lens, S * M * 2u, hipHostMallocDefault)) != hipSuccess ||
@@ -3230,7 +3271,7 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
         (e = hipMalloc((void **)&w.len, (size_t)nblocks * M * 2u)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_slots, w.slots, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_next, w.next, 0)) != hipSuccess ||
-        (e = hipHostGetDevicePointer((void **)&w.d_stop, w.stop, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_ctl, w.ctl, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_ptrs, w.ptrs, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_lens, w.lens, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_q, w.q, 0)) != hipSuccess ||
@@ -3243,7 +3284,7 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
     memset((void *)w.slots, 0, S * sizeof(WorkerSlot));
     for (uint32_t b = 0; b < nblocks; ++b)
         w.next[b] = b + 1u;            // tickets start at 1; block b serves b+1, b+1+B, ...
-    *w.stop = 0;
+    memset((void *)w.ctl, 0, sizeof(WorkerCtl));
     w.out = new yrss_ctx::WorkerState::Out[S];
     for (size_t i = 0; i < S; ++i)
         w.out[i] = yrss_ctx::WorkerState::Out{nullptr, nullptr, nullptr, nullptr, 0u, true};
@@ -3269,7 +3310,6 @@ int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t 
     const uint32_t si = (uint32_t)(t % w.nslots);
     if (!w.out[si].collected)
         return -EBUSY;   // the slot's previous ticket was not polled yet
-    YRSS_HIP(hipSetDevice(c->device));
     WorkerSlot *sl = w.slots + si;
     memcpy(w.ptrs + (size_t)si * kWorkerMaxBurst, ptrs, (size_t)n * 8u);
     if (lens)
@@ -3278,11 +3318,10 @@ int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t 
     sl->flags = flags;
     w.out[si] = yrss_ctx::WorkerState::Out{out_q, out_hash, out_qidx, out_qstart, n, false};
     __atomic_store_n(&sl->seq, t, __ATOMIC_RELEASE);   // n and flags become visible first
+    __atomic_store_n(&w.ctl->pub, t, __ATOMIC_RELAXED);  // ring activity (idle is collective)
     w.issued = t;
     *ticket = t;
-    // no stream query per burst (it costs more than the rest of a submit): a
-    // launch that left while idle is noticed and relaunched by the poll
-    return w.running ? 0 : worker_launch(c);
+    return worker_ensure(c);   // one cached load unless a workgroup left
 }
 
 }  // namespace
@@ -3321,12 +3360,10 @@ int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
         return -EINVAL;   // reused or already collected
     uint64_t spins = 0;
     while (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != ticket) {
-        if ((++spins & 63u) == 0) {
-            YRSS_HIP(hipSetDevice(c->device));
-            int rc = worker_ensure(c);   // the launch may have left while idle
-            if (rc)
-                return rc;
-        }
+        ++spins;
+        const int rc = worker_ensure(c);   // a launch that left: relaunch
+        if (rc)
+            return rc;
         if (!wait)
             return -EAGAIN;
         if (spins > (1ull << 32))
