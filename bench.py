@@ -202,7 +202,8 @@ def probe_traffic(win, lens, out, n, stride, steps):
 def pcie_inclusive(profile: str):
     """Host-resident rates from tools/yrss_cbench (C host over the C ABI):
     DPDK-layout mbuf pool of 2^20 packets in host memory; bursts of 1024 (BASELINE's
-    logical burst) and 32K with two in flight, and 1M."""
+    logical burst) and 32K with two in flight, and 1M; the persistent worker at
+    F-Stack's 32-packet bursts and at 1024."""
     import subprocess
 
     exe = ROOT / "tools" / "yrss_cbench"
@@ -225,13 +226,18 @@ def pcie_inclusive(profile: str):
                 continue
             out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
                         "mpps": d["mpps"], "note": d.get("note", "")})
-    # persistent worker: 32 workgroups, 128 bursts in flight, bursts of 32 and 1024
-    try:
-        r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), "0", "1"],
-                           capture_output=True, text=True, timeout=240,
-                           env={**os.environ, "YRSS_CBENCH_MODES": "4",
-                                "YRSS_CBENCH_WORKER_DEPTH": "128",
-                                "YRSS_CBENCH_WORKER_BLOCKS": "32"})
+    # persistent worker: 64 workgroups, 256 bursts in flight, bursts of 32 and 1024,
+    # mbuf pointers and (data, data_len) pairs
+    for frames in ("0", "1"):
+        try:
+            r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), "0", "1"],
+                               capture_output=True, text=True, timeout=240,
+                               env={**os.environ, "YRSS_CBENCH_MODES": "4",
+                                    "YRSS_CBENCH_WORKER_DEPTH": "256",
+                                    "YRSS_CBENCH_WORKER_BLOCKS": "64",
+                                    "YRSS_CBENCH_WORKER_FRAMES": frames})
+        except subprocess.TimeoutExpired:
+            break
         for line in r.stdout.splitlines():
             try:
                 d = json.loads(line)
@@ -239,8 +245,6 @@ def pcie_inclusive(profile: str):
                 continue
             out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
                         "blocks": d.get("blocks"), "mpps": d["mpps"], "note": d.get("note", "")})
-    except subprocess.TimeoutExpired:
-        pass
     return out or None
 
 

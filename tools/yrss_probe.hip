@@ -12,8 +12,12 @@
 // Its duration on a given box is the practical floor for the parse kernel's
 // traffic there; bench.py reports the parse kernel against it next to the
 // 8 TB/s spec peak, so box-to-box HBM variance is visible.
+// YRSS_PROBE_MODE=1 keeps only the reads (66 B/pkt), =2 only the writes
+// (6 B/pkt), =3 only the writes as 16-byte stores: tools/probe_split.py
+// compares their sum with the mixed run.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -22,12 +26,13 @@ namespace {
 constexpr uint32_t kC = 4;        // tiles per chunk
 constexpr uint32_t kWaves = 8;    // per workgroup (512 threads), one workgroup per CU
 
+template <int kMode>   // 0: reads + writes, 1: reads only, 2: writes only
 __global__ __launch_bounds__(512) void yrss_probe_traffic(const u32x4 *win, const uint16_t *len,
                                                           int16_t *q, uint32_t *hash, uint32_t n)
 {
     __shared__ u32x4 st[kWaves][256];
-    __shared__ uint32_t hb[kWaves][kC * 64];
-    __shared__ uint16_t qb[kWaves][kC * 64];
+    __shared__ __attribute__((aligned(16))) uint32_t hb[kWaves][kC * 64];
+    __shared__ __attribute__((aligned(16))) uint16_t qb[kWaves][kC * 64];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t W = gridDim.x * kWaves;
@@ -37,6 +42,13 @@ __global__ __launch_bounds__(512) void yrss_probe_traffic(const u32x4 *win, cons
     u32x4 nx[4];
     uint16_t nl = 0;
     auto issue = [&](uint32_t t0) {
+        if (kMode >= 2) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                nx[k] = u32x4{t0, lane, (uint32_t)k, n};
+            nl = (uint16_t)t0;
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t p = t0 + 16u * k + (lane >> 2);
@@ -67,8 +79,20 @@ __global__ __launch_bounds__(512) void yrss_probe_traffic(const u32x4 *win, cons
             qb[w][(t - tb) * 64u + lane] = (uint16_t)(x & 0x7fffu);
         }
         const uint32_t base = tb * 64u;
+        if (kMode == 3 && te - tb == kC) {   // writes only, 16 bytes per lane per store
+            __builtin_amdgcn_wave_barrier();
+            reinterpret_cast<u32x4 *>(hash + base)[lane] =
+                reinterpret_cast<const u32x4 *>(hb[w])[lane];
+            if (lane < 32)
+                reinterpret_cast<u32x4 *>(q + base)[lane] =
+                    reinterpret_cast<const u32x4 *>(qb[w])[lane];
+            __builtin_amdgcn_wave_barrier();
+            continue;
+        }
         for (uint32_t j = 0; j < te - tb; ++j) {
             const uint32_t e = j * 64u + lane;
+            if (kMode == 1 && hb[w][e] != 0x9e3779b9u)   // reads only: practically never stores
+                continue;
             if (base + e < n) {
                 hash[base + e] = hb[w][e];
                 q[base + e] = (int16_t)qb[w][e];
@@ -91,7 +115,16 @@ extern "C" int yrss_probe_traffic_launch(const void *win, const void *len, void 
     }
     if (npkts == 0)
         return 0;
-    hipLaunchKernelGGL(yrss_probe_traffic, dim3((unsigned)cus), dim3(512), 0, (hipStream_t)stream,
+    static int mode = -1;
+    if (mode < 0) {
+        const char *e = getenv("YRSS_PROBE_MODE");
+        mode = e ? atoi(e) : 0;
+    }
+    auto k = mode == 1   ? yrss_probe_traffic<1>
+             : mode == 2 ? yrss_probe_traffic<2>
+             : mode == 3 ? yrss_probe_traffic<3>
+                         : yrss_probe_traffic<0>;
+    hipLaunchKernelGGL(k, dim3((unsigned)cus), dim3(512), 0, (hipStream_t)stream,
                        (const u32x4 *)win, (const uint16_t *)len, (int16_t *)q, (uint32_t *)hash,
                        npkts);
     return hipGetLastError() == hipSuccess ? 0 : -5;
