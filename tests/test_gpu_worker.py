@@ -204,3 +204,39 @@ def test_worker_relaunch_nonblocking_poll(dev, oracle_mod, monkeypatch):
             time.sleep(0.02)         # past the idle limit: every workgroup leaves
         eng.worker_stop()
         eng.unregister_host_memory(pool.ctypes.data)
+
+
+def test_worker_then_device_batch(dev, oracle_mod, monkeypatch):
+    """A device-resident batch on the same context retires the resident worker
+    first (its CUs would otherwise stall the batch's grid until the worker
+    idles out); tickets published before it are served after it."""
+    monkeypatch.setenv("YRSS_WORKER_IDLE_MS", "3000")
+    monkeypatch.setenv("YRSS_WORKER_LIFE_MS", "3000")
+    cfg = (3, 3, 1, 1)
+    frames = _frames(oracle_mod, 256, 91)
+    pool, ptrs, _ = _fake_mbufs(frames)
+    q, h, _, _ = _expect(oracle_mod, frames, cfg)
+    n = 1 << 20
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(128, 64)
+        t_a = eng.worker_submit(ptrs[:128])
+        assert eng.worker_poll(t_a) is not None          # the worker is resident now
+        t_b = eng.worker_submit(ptrs[128:256])
+        win, lens = eng.synth(2, n)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = eng.dispatch_dev(win, lens, 64, n)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert dt < 0.5, dt                               # not held up for the 3 s idle limit
+        w_h = win[: 4096 * 64].cpu().numpy()
+        l_h = lens[:4096].cpu().numpy().view(np.uint16)
+        q_ref, h_ref = oracle_mod.dispatch_windows(w_h, 64, l_h, oracle_mod.cfg(*cfg))
+        assert np.array_equal(res.q[:4096].cpu().numpy().view(np.int16), q_ref)
+        assert np.array_equal(res.hash[:4096].cpu().numpy().view(np.uint32), h_ref)
+        r = eng.worker_poll(t_b)                          # relaunched by the poll
+        qi, qs = oracle_mod.process_burst(q[128:256], cfg[1])
+        _check(r, q[128:256], h[128:256], qi, qs)
+        eng.worker_stop()
+        eng.unregister_host_memory(pool.ctypes.data)

@@ -2536,6 +2536,14 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
             YRSS_HIP(hipMemsetAsync(b->qstart, 0, (c->nb + 1) * sizeof(uint32_t), s));
         return 0;
     }
+    // This context's resident worker holds CUs the batch's full grid needs:
+    // retire it first (published tickets stay in the ring; the next worker
+    // submit or poll relaunches).
+    if (c->w.running) {
+        const int rc = worker_halt(c);
+        if (rc)
+            return rc;
+    }
 
     if (c->last_stream_valid && c->last_stream != s) {
         YRSS_HIP(hipEventRecord(c->switch_ev, c->last_stream));
