@@ -259,6 +259,24 @@ int yrss_dispatch_frames(yrss_ctx *ctx, const uint8_t *const *data,
                          uint32_t *out_hash, uint32_t *out_qidx,
                          uint32_t *out_qstart);
 
+/* ---- per-packet registration ------------------------------ */
+
+/* The reference's per-packet hook, unchanged:
+ *   typedef int (*dispatch_func_t)(void *data, uint16_t len, uint16_t queue_id,
+ *                                  uint16_t nb_queues);            fs/lib/ff_api.h:167
+ *   ff_regist_packet_dispatcher(yrss_toeplitz_dispatch);           fs/lib/ff_api.h:170
+ * yrss_toeplitz_dispatch has toeplitz_dispatch's signature and return values
+ * (fs/lib/ff_dpdk_if.c:1945-2113): the target queue, default_Q (2) for unhashed
+ * packets, -1 on error (no context set, a failed GPU call), which F-Stack
+ * answers by freeing the mbuf (ff_dpdk_if.c:1080-1083).  queue_id and
+ * nb_queues are unused, as in the reference.  dispatch_func_t carries no
+ * context, so yrss_set_dispatch_ctx names the one to use (NULL clears it;
+ * yrss_fini clears it for its own context).  Every call is a one-packet GPU
+ * burst with its own launch and synchronisation (~15 µs): a drop-in for
+ * registration, not the fast path — use the burst hook or the worker. */
+int yrss_set_dispatch_ctx(yrss_ctx *ctx);
+int yrss_toeplitz_dispatch(void *data, uint16_t len, uint16_t queue_id, uint16_t nb_queues);
+
 /* ---- burst routing: process_packets' hand-off --------- */
 
 /* Caller-side plumbing, so the routing drives real DPDK objects:

@@ -95,3 +95,12 @@ def test_missing_library_raises(monkeypatch, tmp_path):
     with pytest.raises(abi.YrssLibraryError):
         abi.load()
     monkeypatch.delenv("YRSS_LIB")
+
+
+def test_toeplitz_dispatch_without_context_is_an_error():
+    """The per-packet registration shim with no context: -1, the
+    dispatch_func_t error value (ff_api.h:148-166), and no GPU call."""
+    lib = abi.load()
+    assert lib.yrss_set_dispatch_ctx(None) == 0
+    buf = ctypes.create_string_buffer(64)
+    assert lib.yrss_toeplitz_dispatch(ctypes.cast(buf, ctypes.c_void_p), 64, 0, 3) == -1

@@ -1,0 +1,42 @@
+"""The per-packet registration shim (yrss_toeplitz_dispatch, SURVEY §8(b)
+item 1): called through a dispatch_func_t pointer exactly as F-Stack's
+process_packets calls the registered dispatcher (ff_dpdk_if.c:1078-1079), it
+returns toeplitz_dispatch's value for every packet, from the GPU."""
+import ctypes
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from yastack_amd import SoftRss, abi  # noqa: E402
+
+from test_gpu_small_burst import _expect, _frames  # noqa: E402
+
+DISPATCH_FUNC_T = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint16,
+                                   ctypes.c_uint16, ctypes.c_uint16)
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (5, 4, 1, 0), (4, 2, 0, 1)])
+def test_registered_dispatcher_matches_oracle(dev, oracle_mod, cfg):
+    lib = abi.load()
+    frames = _frames(oracle_mod, 300, 500 + cfg[0])
+    q, _, _, _ = _expect(oracle_mod, frames, cfg)
+    fn = DISPATCH_FUNC_T(ctypes.cast(lib.yrss_toeplitz_dispatch, ctypes.c_void_p).value)
+    with SoftRss(*cfg, device=0) as eng:
+        assert lib.yrss_set_dispatch_ctx(eng._ctx) == 0
+        got = []
+        for j, f in enumerate(frames):
+            buf = ctypes.create_string_buffer(f, len(f))
+            got.append(fn(ctypes.cast(buf, ctypes.c_void_p), len(f), j % 7, cfg[1]))
+        assert np.array_equal(np.array(got, np.int16), q)
+    # yrss_fini cleared the context it owned: back to the error value
+    buf = ctypes.create_string_buffer(frames[0], len(frames[0]))
+    assert fn(ctypes.cast(buf, ctypes.c_void_p), len(frames[0]), 0, cfg[1]) == -1

@@ -158,6 +158,9 @@ _PROTOS = {
     "yrss_worker_stop": (ctypes.c_int, [_vp]),
     "yrss_dispatch_frames_zc_ex": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp,
                                                   _u32]),
+    "yrss_set_dispatch_ctx": (ctypes.c_int, [_vp]),
+    "yrss_toeplitz_dispatch": (ctypes.c_int, [_vp, ctypes.c_uint16, ctypes.c_uint16,
+                                              ctypes.c_uint16]),
     "yrss_set_kni": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p,
                                     ctypes.c_char_p]),
     "yrss_dispatch_dev_ex": (ctypes.c_int, [_vp, ctypes.POINTER(DevBatch), _vp]),

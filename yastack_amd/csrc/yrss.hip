@@ -2101,6 +2101,10 @@ void host_reg_release(void *base)
 int worker_halt(yrss_ctx *c);
 void worker_free(yrss_ctx *c);
 
+// Context behind yrss_toeplitz_dispatch: dispatch_func_t has no context
+// argument (ff_api.h:167), so the registration shim reads this one.
+yrss_ctx *g_dispatch_ctx = nullptr;
+
 // A scan look-back that never resolved leaves that batch's lists invalid.
 bool take_scan_fault(yrss_ctx *c)
 {
@@ -2442,6 +2446,9 @@ void yrss_fini(yrss_ctx *c)
     if (!c)
         return;
     (void)hipSetDevice(c->device);
+    yrss_ctx *self = c;
+    __atomic_compare_exchange_n(&g_dispatch_ctx, &self, (yrss_ctx *)nullptr, false,
+                                __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
     if (c->w.on) {
         (void)worker_halt(c);
         worker_free(c);
@@ -2701,6 +2708,38 @@ int yrss_dispatch_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t
                               false)) != 0)
         return rc;
     return finish_burst(c);
+}
+
+int yrss_set_dispatch_ctx(yrss_ctx *c)
+{
+    __atomic_store_n(&g_dispatch_ctx, c, __ATOMIC_RELEASE);
+    return 0;
+}
+
+// toeplitz_dispatch's own signature (ff_dpdk_if.c:1945-1946), so it can be
+// handed to ff_regist_packet_dispatcher unchanged.  Each call is a one-packet
+// burst through the GPU (yrss_burst_small), bit-identical to the reference,
+// but it pays a launch and a synchronisation per packet: the burst hook is
+// the fast path.  queue_id and nb_queues are unused, as in the reference.
+int yrss_toeplitz_dispatch(void *data, uint16_t len, uint16_t queue_id, uint16_t nb_queues)
+{
+    (void)queue_id;
+    (void)nb_queues;
+    yrss_ctx *c = __atomic_load_n(&g_dispatch_ctx, __ATOMIC_ACQUIRE);
+    if (!c || !data) {
+        // the contract's only error channel (ff_api.h:148-166): F-Stack frees the mbuf
+        static bool warned = false;
+        if (!c && !warned) {
+            warned = true;
+            fprintf(stderr, "yrss: yrss_toeplitz_dispatch without yrss_set_dispatch_ctx\n");
+        }
+        return -1;
+    }
+    const uint8_t *d = static_cast<const uint8_t *>(data);
+    int16_t q = 0;
+    if (yrss_dispatch_frames(c, &d, &len, 1u, &q, nullptr, nullptr, nullptr) != 0)
+        return -1;
+    return q;
 }
 
 int yrss_dispatch_burst(yrss_ctx *c, void *const *mbufs, uint32_t n, int16_t *out_q,
