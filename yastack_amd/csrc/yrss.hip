@@ -2259,22 +2259,34 @@ int gather_mbufs(yrss_ctx *c, void *const *mbufs, uint32_t n, uint32_t *W_out)
     if (rc)
         return rc;
     const yrss_mbuf_layout &ml = c->cfg.mbuf;
+    // Two passes, both bound by host memory latency (cache-cold mbufs): the
+    // first reads each header (data_len decides the window stride, and the
+    // window's address is kept in the pinned pointer scratch), the second
+    // copies the windows.  Each pass prefetches kGatherAhead packets ahead.
+    constexpr uint32_t kGatherAhead = 16;
+    const uint8_t **src = reinterpret_cast<const uint8_t **>(c->h_ptrs);
     uint32_t maxlen = 0;
     for (uint32_t i = 0; i < n; ++i) {
-        uint16_t L;
-        memcpy(&L, (const uint8_t *)mbufs[i] + ml.off_data_len, 2);
+        if (i + kGatherAhead < n)
+            __builtin_prefetch((const uint8_t *)mbufs[i + kGatherAhead]);
+        const uint8_t *m = (const uint8_t *)mbufs[i];
+        const uint8_t *buf;
+        uint16_t doff, L;
+        memcpy(&buf, m + ml.off_buf_addr, sizeof(buf));
+        memcpy(&doff, m + ml.off_data_off, 2);
+        memcpy(&L, m + ml.off_data_len, 2);
+        src[i] = buf + doff;
         c->h_len[i] = L;
         maxlen = std::max<uint32_t>(maxlen, L);
     }
     const uint32_t W = host_stride(maxlen);
     for (uint32_t i = 0; i < n; ++i) {
-        const uint8_t *m = (const uint8_t *)mbufs[i];
-        const uint8_t *buf;
-        uint16_t doff;
-        memcpy(&buf, m + ml.off_buf_addr, sizeof(buf));
-        memcpy(&doff, m + ml.off_data_off, 2);
+        if (i + kGatherAhead < n) {
+            __builtin_prefetch(src[i + kGatherAhead]);
+            __builtin_prefetch(src[i + kGatherAhead] + W - 1);
+        }
         const uint32_t L = c->h_len[i];
-        memcpy(c->h_win + (size_t)i * W, buf + doff, L < W ? L : W);
+        memcpy(c->h_win + (size_t)i * W, src[i], L < W ? L : W);
     }
     *W_out = W;
     return 0;
@@ -2700,6 +2712,8 @@ int yrss_dispatch_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t
         maxlen = std::max<uint32_t>(maxlen, len[i]);
     const uint32_t W = host_stride(maxlen);
     for (uint32_t i = 0; i < n; ++i) {
+        if (i + 16u < n)
+            __builtin_prefetch(data[i + 16u]);
         const uint32_t L = len[i];
         memcpy(c->h_win + (size_t)i * W, data[i], L < W ? L : W);
         c->h_len[i] = (uint16_t)L;
