@@ -419,7 +419,8 @@ int yrss_worker_submit_frames(yrss_ctx *ctx, const uint8_t *const *data, const u
                               uint32_t n, int16_t *out_q, uint32_t *out_hash,
                               uint32_t *out_qidx, uint32_t *out_qstart, uint64_t *ticket);
 /* 0: the burst is done and its outputs copied; -EAGAIN: not yet (wait = 0);
- * -EFAULT: a mbuf or its data lies outside every registered range. */
+ * -EFAULT: a mbuf or its data lies outside every registered range;
+ * -ETIMEDOUT: waited 10 s (a burst takes microseconds: the GPU is hung). */
 int yrss_worker_poll(yrss_ctx *ctx, uint64_t ticket, int wait);
 /* Stop the kernel and free the ring (also done by yrss_fini). */
 int yrss_worker_stop(yrss_ctx *ctx);

@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <strings.h>
+#include <time.h>
 
 #include <map>
 #include <mutex>
@@ -2101,6 +2102,13 @@ void host_reg_release(void *base)
 int worker_halt(yrss_ctx *c);
 void worker_free(yrss_ctx *c);
 
+uint64_t mono_ns()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
 // Context behind yrss_toeplitz_dispatch: dispatch_func_t has no context
 // argument (ff_api.h:167), so the registration shim reads this one.
 yrss_ctx *g_dispatch_ctx = nullptr;
@@ -3382,7 +3390,10 @@ int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t 
     __atomic_store_n(&w.ctl->pub, t, __ATOMIC_RELAXED);  // ring activity (idle is collective)
     w.issued = t;
     *ticket = t;
-    return worker_ensure(c);   // one cached load unless a workgroup left
+    const int rc = worker_ensure(c);   // one cached load unless a workgroup left
+    if (rc)
+        w.out[si].collected = true;    // no launch serves it: the slot is free again
+    return rc;
 }
 
 }  // namespace
@@ -3419,16 +3430,20 @@ int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
     auto &o = w.out[si];
     if (ticket + w.nslots <= w.issued || o.collected)
         return -EINVAL;   // reused or already collected
-    uint64_t spins = 0;
+    uint64_t spins = 0, t0 = 0;
     while (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != ticket) {
-        ++spins;
         const int rc = worker_ensure(c);   // a launch that left: relaunch
         if (rc)
             return rc;
         if (!wait)
             return -EAGAIN;
-        if (spins > (1ull << 32))
-            return -ETIMEDOUT;
+        if ((++spins & 4095u) == 0) {       // a burst takes microseconds: 10 s is a hung GPU
+            const uint64_t now = mono_ns();
+            if (!t0)
+                t0 = now;
+            else if (now - t0 > 10ull * 1000000000ull)
+                return -ETIMEDOUT;
+        }
         __builtin_ia32_pause();
     }
     o.collected = true;
