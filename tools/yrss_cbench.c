@@ -123,10 +123,11 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
            "\"burst\": %u, \"inflight\": %u, \"blocks\": %u, \"pkts\": %llu, "
            "\"seconds\": %.3f, \"mpps\": %.2f, \"us_per_burst\": %.2f, \"thp\": %d, "
            "\"mode\": 4, \"note\": \"persistent kernel polls a ring of bursts in pinned "
-           "memory; mbufs read over PCIe\"}\n",
+           "memory; %s read over PCIe\"}\n",
            frames ? "yrss_worker_submit_frames" : "yrss_worker_submit", profile, B, depth,
            blocks, (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
-           (t1 - t0) / (pkts / (double)B) * 1e6, thp);
+           (t1 - t0) / (pkts / (double)B) * 1e6, thp,
+           frames ? "windows of (data, data_len) pairs" : "mbuf headers + windows");
     fflush(stdout);
     free(tk);
     yrss_fini(ctx);
