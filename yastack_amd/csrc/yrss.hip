@@ -1306,6 +1306,8 @@ struct SmallParams {
     uint32_t *qstart;    // host-visible [nb + 1], or null
     uint32_t gather;     // 1: gather the windows first (zero-copy modes)
     uint32_t writeback;  // 1: store hash.rss into each mbuf (YRSS_F_WRITE_RSS)
+    uint64_t *done;      // host-coherent completion word, or null
+    uint64_t seq;        // stored into *done once every output is visible to the host
 };
 
 __host__ __device__ inline size_t small_lds(uint32_t nb, bool filter)
@@ -1370,6 +1372,8 @@ struct BurstIO {
     uint32_t *qstart;    // host-visible [nb + 1], or null
     uint32_t gather;     // 1: gather the windows first (zero-copy modes)
     uint32_t writeback;  // 1: store hash.rss into each mbuf (YRSS_F_WRITE_RSS)
+    uint64_t *done;      // host-coherent completion word, or null
+    uint64_t seq;        // stored into *done once every output is visible to the host
 };
 
 template <bool kFilter, uint32_t kTW = kOutTiles>   // kTW: tiles per wave (n <= kTW * 1024)
@@ -1465,6 +1469,17 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
     small_burst_body<kFilter>(S.P, S.G, gather_io(S.G),
                               BurstIO{S.qidx, S.qstart, S.gather, S.writeback}, L, wave,
                               lane_id());
+    if (S.done) {
+        // the host spins on this word instead of a stream synchronisation:
+        // every wave's stores drained, one system-scope release, then the word
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(S.done, S.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1703,6 +1718,7 @@ struct PendingBurst {
     HostOut outs[5] = {};            // q, hash, qidx, qstart, filter
     bool gather_fault = false;       // zero-copy: a pointer outside every range
     bool scan_fault = false;         // multi-kernel path: scan look-back fault
+    uint64_t done_seq = 0;           // one-launch path: value the kernel stores in *h_done
     void *const *wb_mbufs = nullptr; // host-side hash.rss write-back (staged path)
 };
 
@@ -1763,6 +1779,10 @@ struct yrss_ctx {
     uint64_t *d_ptrs = nullptr;
     uint32_t *d_fault = nullptr;
     uint32_t *h_fault = nullptr;    // host-coherent
+    uint64_t *h_done = nullptr;     // host-coherent completion word of yrss_burst_small
+    uint64_t *dh_done = nullptr;
+    uint64_t done_seq = 0;
+    bool spin_wait = true;          // YRSS_SPIN_WAIT=0: always hipStreamSynchronize
     // device views of the pinned staging: the small-burst kernel reads and
     // writes it in place (no copies)
     bool no_small = false;          // YRSS_NO_SMALL: always the multi-kernel path
@@ -2145,6 +2165,9 @@ int small_launch(yrss_ctx *c, SmallParams &S, bool filter)
     P.rank = nullptr;
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
+    S.done = c->spin_wait ? c->dh_done : nullptr;
+    S.seq = ++c->done_seq;
+    c->pend.done_seq = c->spin_wait ? S.seq : 0u;   // the caller reset pend before
     const size_t lds = small_lds(c->nb, filter);
     const dim3 grid(1);
     if (filter)
@@ -2163,7 +2186,24 @@ int finish_burst(yrss_ctx *c)
     if (!p.active)
         return 0;
     p.active = false;
-    YRSS_HIP(hipStreamSynchronize(c->stream));
+    // One-launch bursts publish a completion word: spin on it (a stream
+    // synchronisation costs microseconds of wake-up on top of the kernel);
+    // anything else, or a word that does not come, takes the stream sync.
+    bool done = false;
+    if (p.done_seq) {
+        const uint64_t t0 = mono_ns();
+        for (uint32_t k = 1;; ++k) {
+            if (__atomic_load_n(c->h_done, __ATOMIC_ACQUIRE) == p.done_seq) {
+                done = true;
+                break;
+            }
+            if ((k & 255u) == 0 && mono_ns() - t0 > 2000000ull)   // 2 ms
+                break;
+            __builtin_ia32_pause();
+        }
+    }
+    if (!done)
+        YRSS_HIP(hipStreamSynchronize(c->stream));
     if (p.gather_fault && __atomic_load_n(c->h_fault, __ATOMIC_ACQUIRE))
         return -EFAULT;
     if (p.scan_fault && take_scan_fault(c))
@@ -2409,6 +2449,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         c->proto.out16 = (uint32_t)std::min(2, std::max(0, atoi(e)));
     if (const char *e = getenv("YRSS_NO_SMALL"))
         c->no_small = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_SPIN_WAIT"))   // A/B: spin vs stream sync
+        c->spin_wait = atoi(e) != 0;
     if (const char *e = getenv("YRSS_EVENT_FLAGS"))   // A/B of the timing-event fence
         c->event_flags = (unsigned)strtoul(e, nullptr, 0);
     c->nb = (uint32_t)cfg->nb_queues + 1u;
@@ -2437,6 +2479,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         (e = hipHostMalloc((void **)&c->h_fault, sizeof(uint32_t), hipHostMallocCoherent)) !=
             hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&c->dh_fault, c->h_fault, 0)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&c->h_done, 64, hipHostMallocCoherent)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&c->dh_done, c->h_done, 0)) != hipSuccess ||
         (e = hipMemset(c->d_kni, 0, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipMemset(c->d_seg_cnt, 0, ws)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
@@ -2445,6 +2489,7 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         return hip_fail("yrss_init allocation", e);
     }
     *c->d_scan_fault = 0;
+    *c->h_done = 0;
     // The memsets above run on the null stream, which does not order against
     // the context's non-blocking stream: without this wait a first dispatch
     // could race the zeroing of the count matrix (seen once on the GPU box as
@@ -2493,6 +2538,7 @@ void yrss_fini(yrss_ctx *c)
     (void)hipFree(c->d_kni);
     (void)hipFree(c->d_fault);
     (void)hipHostFree(c->h_fault);
+    (void)hipHostFree(c->h_done);
     for (uint32_t r = 0; r < c->nranges; ++r)
         host_reg_release(c->range_base[r]);
     if (c->switch_ev)
