@@ -248,7 +248,9 @@ int yrss_dispatch_frames_zc_ex(yrss_ctx *ctx, const uint8_t *const *data, const 
 int yrss_wait(yrss_ctx *ctx);
 
 /* Register / unregister a host range (hipHostRegister, mapped) for the
- * zero-copy path; up to 16 ranges per context. */
+ * zero-copy path; up to 16 ranges per context.  Unregistering returns -EBUSY
+ * while a persistent-worker burst of the context is pending (not yet polled):
+ * it may still read mbufs or write outputs in that range. */
 #define YRSS_MAX_HOST_RANGES 16
 int yrss_register_host_memory(yrss_ctx *ctx, void *base, size_t len);
 int yrss_unregister_host_memory(yrss_ctx *ctx, void *base);
@@ -392,9 +394,10 @@ int yrss_timing_read(yrss_ctx *ctx, int kernel, double *total_ms,
  * a persistent gfx950 kernel (nblocks workgroups, one CU each) polls a ring of
  * nslots slots in host-coherent pinned memory.  Submit copies the mbuf pointer
  * array into a slot and publishes it; the kernel reads the mbufs (which must
- * lie in memory registered with yrss_register_host_memory) over PCIe,
- * classifies them like yrss_dispatch_burst_zc and writes the results into the
- * slot; poll copies them to the caller's arrays.  Up to nslots bursts are in
+ * lie in memory registered with yrss_register_host_memory) over PCIe and
+ * classifies them like yrss_dispatch_burst_zc.  Output arrays that lie in
+ * registered memory are written in place; others are written into the slot
+ * and copied to the caller's arrays by the poll.  Up to nslots bursts are in
  * flight; every ticket must be polled before its slot is reused (submit
  * returns -EBUSY otherwise).  The kernel leaves after YRSS_WORKER_IDLE_MS
  * (default 50) without a submit or YRSS_WORKER_LIFE_MS (default 1000) in total
@@ -418,7 +421,7 @@ int yrss_worker_submit(yrss_ctx *ctx, void *const *mbufs, uint32_t n, int16_t *o
 int yrss_worker_submit_frames(yrss_ctx *ctx, const uint8_t *const *data, const uint16_t *len,
                               uint32_t n, int16_t *out_q, uint32_t *out_hash,
                               uint32_t *out_qidx, uint32_t *out_qstart, uint64_t *ticket);
-/* 0: the burst is done and its outputs copied; -EAGAIN: not yet (wait = 0);
+/* 0: the burst is done and its outputs in place; -EAGAIN: not yet (wait = 0);
  * -EFAULT: a mbuf or its data lies outside every registered range;
  * -ETIMEDOUT: waited 10 s (a burst takes microseconds: the GPU is hung). */
 int yrss_worker_poll(yrss_ctx *ctx, uint64_t ticket, int wait);

@@ -240,3 +240,58 @@ def test_worker_then_device_batch(dev, oracle_mod, monkeypatch):
         _check(r, q[128:256], h[128:256], qi, qs)
         eng.worker_stop()
         eng.unregister_host_memory(pool.ctypes.data)
+
+
+def test_worker_direct_outputs(dev, oracle_mod):
+    """Output arrays inside registered host memory are written by the GPU in
+    place (the poll copies nothing); arrays outside go through the slot's
+    staging; both match the oracle, also mixed within one burst.  A registered
+    range a pending burst may touch cannot be unregistered (-EBUSY)."""
+    cfg = (5, 4, 1, 1)
+    sizes = [32, 1024, 7, 500, 32, 1]
+    frames = _frames(oracle_mod, sum(sizes), 66)
+    pool, ptrs, _ = _fake_mbufs(frames)
+    q_all, h_all, _, _ = _expect(oracle_mod, frames, cfg)
+    lib = abi.load()
+    arena = np.zeros(1 << 20, np.uint8)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.register_host_memory(arena.ctypes.data, arena.nbytes)
+        eng.worker_start(8, 2)
+        off, pend = 0, []
+        nonlocal_pos = [0]
+        for i, n in enumerate(sizes):
+            m = max(n, 1)
+            # even bursts: every output in the registered arena; odd: q and
+            # qstart there, hash and qidx in plain (unregistered) arrays
+            def take(nbytes, dtype):
+                nonlocal_pos[0] = (nonlocal_pos[0] + 63) & ~63
+                a = arena[nonlocal_pos[0]:nonlocal_pos[0] + nbytes].view(dtype)
+                nonlocal_pos[0] += nbytes
+                return a
+            q = take(2 * m, np.int16)
+            qs = take(4 * (cfg[1] + 2), np.uint32)
+            if i % 2 == 0:
+                h = take(4 * m, np.uint32)
+                qi = take(4 * m, np.uint32)
+            else:
+                h = np.zeros(m, np.uint32)
+                qi = np.zeros(m, np.uint32)
+            t = ctypes.c_uint64()
+            mb = np.ascontiguousarray(ptrs[off:off + n])
+            assert lib.yrss_worker_submit(eng._ctx, mb.ctypes.data, n, q.ctypes.data,
+                                          h.ctypes.data, qi.ctypes.data, qs.ctypes.data, 0,
+                                          ctypes.byref(t)) == 0
+            pend.append((t.value, off, n, q, h, qi, qs))
+            off += n
+        assert lib.yrss_unregister_host_memory(eng._ctx, arena.ctypes.data) == -16   # EBUSY
+        for t, o, n, q, h, qi, qs in pend:
+            assert lib.yrss_worker_poll(eng._ctx, t, 1) == 0
+            qr = q_all[o:o + n]
+            qi_ref, qs_ref = oracle_mod.process_burst(qr, cfg[1])
+            assert np.array_equal(q[:n], qr) and np.array_equal(h[:n], h_all[o:o + n])
+            assert np.array_equal(qi[:n], qi_ref)
+            assert np.array_equal(qs[: qs_ref.size], qs_ref)
+        eng.worker_stop()
+        eng.unregister_host_memory(arena.ctypes.data)
+        eng.unregister_host_memory(pool.ctypes.data)

@@ -9,5 +9,8 @@ for path in sys.argv[1:]:
             d = json.loads(line)
         except ValueError:
             continue
-        print("%-26s burst %7d inflight %d %9.2f Mpkt/s %9.2f us/burst"
-              % (d["api"], d["burst"], d.get("inflight", 1), d["mpps"], d["us_per_burst"]))
+        extra = ""
+        if "poll_cycles" in d:   # host TSC cycles per burst inside poll / submit
+            extra = "  poll %5.0f cyc  submit %5.0f cyc" % (d["poll_cycles"], d["submit_cycles"])
+        print("%-26s burst %7d inflight %d %9.2f Mpkt/s %9.2f us/burst%s"
+              % (d["api"], d["burst"], d.get("inflight", 1), d["mpps"], d["us_per_burst"], extra))

@@ -1,0 +1,12 @@
+# Persistent worker at 32-packet bursts: where the dispatcher thread's time
+# goes (TSC cycles inside yrss_worker_poll / _submit per burst), and the
+# protocol ceiling with empty bursts (n = 0 moves no packets: rate in bursts).
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+for fr in 1 0; do
+  for b in 16 64 128; do
+    d=$((b * 4))
+    YRSS_CBENCH_WORKER_FRAMES=$fr YRSS_CBENCH_MODES=4 YRSS_CBENCH_WORKER_DEPTH=$d YRSS_CBENCH_WORKER_BLOCKS=$b timeout -k 10 120 tools/yrss_cbench 1 1048576 32 1 > gpurun_out/cbw.log 2>&1 || { cat gpurun_out/cbw.log; exit 1; }
+    python3 tools/cb_summary.py gpurun_out/cbw.log | sed "s/\$/  blocks $b/"
+  done
+done

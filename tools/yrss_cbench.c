@@ -18,6 +18,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <time.h>
+#include <x86intrin.h>
 
 #include "yrss.h"
 #include "yrss_synth.h"
@@ -83,7 +84,7 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
     }
     static uint32_t qs[YRSS_WORKER_MAX_SLOTS][YRSS_MAX_QUEUES + 2];
     uint64_t *tk = calloc(depth, sizeof(uint64_t));
-    uint64_t pkts = 0, i = 0;
+    uint64_t pkts = 0, i = 0, cyc_poll = 0, cyc_sub = 0, nb = 0;
     uint32_t off = 0;
     double t0 = 0, t1 = 0;
     for (int pass = 0; pass < 2; ++pass) {          /* pass 0: warm-up */
@@ -91,18 +92,24 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
         t0 = now();
         t1 = t0;
         pkts = 0;
+        cyc_poll = cyc_sub = nb = 0;
         while (t1 - t0 < lim) {
             if (off + B > pool)
                 off = 0;
             const unsigned k = (unsigned)(i % depth);
+            const uint64_t c0 = __rdtsc();
             if (i >= depth && (rc = yrss_worker_poll(ctx, tk[k], 1)) != 0) {
                 fprintf(stderr, "worker poll: %d\n", rc);
                 return 3;
             }
+            const uint64_t c1 = __rdtsc();
             rc = frames ? yrss_worker_submit_frames(ctx, fdata + off, flen + off, B, q_all + off,
                                                     h_all + off, qi_all + off, qs[k], &tk[k])
                         : yrss_worker_submit(ctx, mbufs + off, B, q_all + off, h_all + off,
                                              qi_all + off, qs[k], 0, &tk[k]);
+            cyc_poll += c1 - c0;
+            cyc_sub += __rdtsc() - c1;
+            ++nb;
             if (rc != 0) {
                 fprintf(stderr, "worker submit: %d\n", rc);
                 return 3;
@@ -110,7 +117,8 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
             ++i;
             off += B;
             pkts += B;
-            t1 = now();
+            if ((i & 63u) == 0)   /* the clock read is not part of a burst's cost */
+                t1 = now();
         }
     }
     for (uint64_t j = i > depth ? i - depth : 0; j < i; ++j)
@@ -122,11 +130,13 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
     printf("{\"tool\": \"yrss_cbench\", \"api\": \"%s\", \"profile\": %u, "
            "\"burst\": %u, \"inflight\": %u, \"blocks\": %u, \"pkts\": %llu, "
            "\"seconds\": %.3f, \"mpps\": %.2f, \"us_per_burst\": %.2f, \"thp\": %d, "
+           "\"poll_cycles\": %.0f, \"submit_cycles\": %.0f, "
            "\"mode\": 4, \"note\": \"persistent kernel polls a ring of bursts in pinned "
            "memory; %s read over PCIe\"}\n",
            frames ? "yrss_worker_submit_frames" : "yrss_worker_submit", profile, B, depth,
            blocks, (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
-           (t1 - t0) / (pkts / (double)B) * 1e6, thp,
+           (t1 - t0) / (pkts / (double)B) * 1e6, thp, nb ? (double)cyc_poll / nb : 0.0,
+           nb ? (double)cyc_sub / nb : 0.0,
            frames ? "windows of (data, data_len) pairs" : "mbuf headers + windows");
     fflush(stdout);
     free(tk);

@@ -1503,14 +1503,22 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
 // ---------------------------------------------------------------------------
 constexpr uint32_t kWorkerMaxBurst = YRSS_WORKER_MAX_BURST;   // 16 tiles: one per wave
 
+// Written by the host only, so its submit stores stay cache hits; the GPU
+// answers in a separate done array (WorkerParams::done).
 struct alignas(64) WorkerSlot {
-    uint64_t seq;        // host: ticket, written last (release)
-    uint32_t n;          // host: packets (written before seq; read with it, one 16-B load)
-    uint32_t flags;      // host: YRSS_F_WRITE_RSS | kWorkerFrames
-    uint64_t done;       // GPU: ticket, written after the outputs (release, system)
-    uint32_t fault;      // GPU: a pointer outside every registered range
-    uint32_t pad_[9];
+    uint64_t seq;        // ticket, written last (release)
+    uint32_t n;          // packets (written before seq; read with it, one 16-B load)
+    uint32_t flags;      // YRSS_F_WRITE_RSS | kWorkerFrames
+    // device addresses of q, hash, qidx, qstart (read after the acquire): the
+    // caller's own arrays when they lie in registered memory (no copy at
+    // poll), else the slot's staging; 0 = not wanted
+    uint64_t out[4];
+    uint64_t pad_[2];
 };
+// done[slot] = ticket | kWorkerFault when a pointer was outside every range.
+// Consecutive slots share a line, so a host polling in ticket order misses
+// once per eight bursts instead of once per burst.
+constexpr uint64_t kWorkerFault = 1ull << 63;
 constexpr uint32_t kWorkerFrames = 1u << 16;   // slot holds (data, data_len) pairs
 static_assert(sizeof(WorkerSlot) == 64, "one line per slot header");
 
@@ -1529,21 +1537,19 @@ static_assert(sizeof(WorkerCtl) == 128, "two lines");
 struct WorkerParams {
     ParseParams P;       // configuration (per-burst fields set in the kernel)
     GatherParams G;      // range table and mbuf layout
-    WorkerSlot *slots;   // [nslots] host-coherent
+    WorkerSlot *slots;   // [nslots] host-coherent, host-written
+    uint64_t *done;      // [nslots] host-coherent, GPU-written
+    uint32_t *fault;     // [nblocks] device: gather fault of the current burst
     uint64_t *ptrs;      // [nslots][kWorkerMaxBurst] pinned: mbuf or frame data pointers
     uint16_t *lens;      // [nslots][kWorkerMaxBurst] pinned: frame data_len (frames mode)
-    int16_t *q;          // [nslots][kWorkerMaxBurst] pinned outputs
-    uint32_t *hash;
-    uint32_t *qidx;
-    uint32_t *qstart;    // [nslots][qs_stride]
     uint8_t *win;        // device scratch [nblocks][kWorkerMaxBurst * 80]
     uint16_t *len;       // device scratch [nblocks][kWorkerMaxBurst]
     uint64_t *next;      // host-coherent [nblocks]: ticket to serve next (resume)
     WorkerCtl *wctl;     // host-coherent launch control
     uint32_t nslots;
-    uint32_t qs_stride;
     uint64_t idle_ticks; // s_memrealtime ticks (100 MHz)
     uint64_t life_ticks;
+    uint32_t poll_sleep; // s_sleep(2) units between two polls of a slot
 };
 
 size_t worker_lds(uint32_t nb) { return small_lds(nb, false) + 64u; }
@@ -1600,11 +1606,25 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
                     pub_seen = pub;
                     t_last = now;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                // each poll is a PCIe read: many resident workgroups polling
+                // back to back compete with the bursts' own reads
+                for (uint32_t z = 0; z < W.poll_sleep; ++z)
+                    __builtin_amdgcn_s_sleep(2);
             }
             if (go == 1) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                __hip_atomic_store(&sl->fault, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(W.fault + blockIdx.x, 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                uint64_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    o[k] = __hip_atomic_load(&sl->out[k], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    ctl[4 + 2 * k] = (uint32_t)o[k];
+                    ctl[5 + 2 * k] = (uint32_t)(o[k] >> 32);
+                }
             }
             ctl[0] = go;
         }
@@ -1617,8 +1637,11 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         P.win = W.win + (size_t)blockIdx.x * kWorkerMaxBurst * YRSS_WIN_FULL;
         P.len = W.len + (size_t)blockIdx.x * kWorkerMaxBurst;
         P.stride = YRSS_WIN_FULL;
-        P.q = W.q + (size_t)si * kWorkerMaxBurst;
-        P.hash = W.hash + (size_t)si * kWorkerMaxBurst;
+        auto out_ptr = [&](int k) {
+            return (void *)(uintptr_t)(((uint64_t)ctl[5 + 2 * k] << 32) | ctl[4 + 2 * k]);
+        };
+        P.q = static_cast<int16_t *>(out_ptr(0));
+        P.hash = static_cast<uint32_t *>(out_ptr(1));
         P.filter = nullptr;
         P.rank = nullptr;
         P.seg_cnt = nullptr;
@@ -1626,15 +1649,15 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         const uint32_t frames = (ctl[2] & kWorkerFrames) ? 1u : 0u;
         const GatherIO gio{W.ptrs + (size_t)si * kWorkerMaxBurst,
                            W.lens + (size_t)si * kWorkerMaxBurst, const_cast<uint8_t *>(P.win),
-                           const_cast<uint16_t *>(P.len), &sl->fault, n, frames};
+                           const_cast<uint16_t *>(P.len), W.fault + blockIdx.x, n, frames};
         if (n) {
             small_burst_body<false, 1>(P, W.G, gio,
-                                    BurstIO{W.qidx + (size_t)si * kWorkerMaxBurst,
-                                            W.qstart + (size_t)si * W.qs_stride, 1u,
+                                    BurstIO{static_cast<uint32_t *>(out_ptr(2)),
+                                            static_cast<uint32_t *>(out_ptr(3)), 1u,
                                             (!frames && (ctl[2] & YRSS_F_WRITE_RSS)) ? 1u : 0u},
                                     L, wave, lane);
-        } else if (threadIdx.x <= W.P.nb) {
-            W.qstart[(size_t)si * W.qs_stride + threadIdx.x] = 0u;
+        } else if (threadIdx.x <= W.P.nb && out_ptr(3)) {
+            static_cast<uint32_t *>(out_ptr(3))[threadIdx.x] = 0u;
         }
         // every wave's output stores drained, then one system-scope release
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1642,7 +1665,10 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         if (threadIdx.x == 0) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&sl->done, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint32_t f = __hip_atomic_load(W.fault + blockIdx.x, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(W.done + si, t | (f ? kWorkerFault : 0ull), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
         }
         t_last = wall_clock64();
         t += gridDim.x;
@@ -1802,8 +1828,11 @@ struct yrss_ctx {
         bool running = false;      // a worker launch may still be in flight
         uint32_t nslots = 0, nblocks = 0, qs_stride = 0;
         uint64_t idle_ticks = 0, life_ticks = 0;
+        uint32_t poll_sleep = 1;
         hipStream_t stream = nullptr;
         WorkerSlot *slots = nullptr, *d_slots = nullptr;   // host-coherent
+        uint64_t *done = nullptr, *d_done = nullptr;       // host-coherent
+        uint32_t *fault = nullptr;                         // device [nblocks]
         uint64_t *ptrs = nullptr, *d_ptrs = nullptr;       // pinned
         uint16_t *lens = nullptr, *d_lens = nullptr;       // pinned (frames mode)
         int16_t *q = nullptr, *d_q = nullptr;
@@ -1815,11 +1844,13 @@ struct yrss_ctx {
         uint8_t *win = nullptr;                            // device scratch
         uint16_t *len = nullptr;
         uint64_t issued = 0;       // last ticket handed out
+        uint32_t pending = 0;      // submitted, not yet polled
         struct Out {
             int16_t *q;
             uint32_t *hash, *qidx, *qstart;
             uint32_t n;
             bool collected;
+            uint8_t copy;          // bit k: output k comes from the slot's staging
         } *out = nullptr;          // [nslots]
     } w;
     // The compaction workspace is shared by every dispatch of the context; a
@@ -2865,6 +2896,9 @@ int yrss_unregister_host_memory(yrss_ctx *c, void *base)
         return -EINVAL;
     for (uint32_t r = 0; r < c->nranges; ++r)
         if (c->range_base[r] == base) {
+            // a pending worker burst may read mbufs or write outputs there
+            if (c->w.on && c->w.pending)
+                return -EBUSY;
             YRSS_HIP(hipSetDevice(c->device));
             const int hrc = worker_halt(c);
             if (hrc)
@@ -3256,6 +3290,8 @@ void worker_free(yrss_ctx *c)
 {
     auto &w = c->w;
     (void)hipHostFree(w.slots);
+    (void)hipHostFree(w.done);
+    (void)hipFree(w.fault);
     (void)hipHostFree(w.ptrs);
     (void)hipHostFree(w.lens);
     (void)hipHostFree(w.q);
@@ -3304,20 +3340,18 @@ int worker_launch(yrss_ctx *c)
     W.G.off_hash_rss = ml.off_hash_rss;
     memcpy(W.G.ranges, c->ranges, sizeof(W.G.ranges));
     W.slots = w.d_slots;
+    W.done = w.d_done;
+    W.fault = w.fault;
     W.ptrs = w.d_ptrs;
     W.lens = w.d_lens;
-    W.q = w.d_q;
-    W.hash = w.d_hash;
-    W.qidx = w.d_qidx;
-    W.qstart = w.d_qstart;
     W.win = w.win;
     W.len = w.len;
     W.next = w.d_next;
     W.wctl = w.d_ctl;
     W.nslots = w.nslots;
-    W.qs_stride = w.qs_stride;
     W.idle_ticks = w.idle_ticks;
     W.life_ticks = w.life_ticks;
+    W.poll_sleep = w.poll_sleep;
     hipLaunchKernelGGL(yrss_burst_worker, dim3(w.nblocks), dim3(kSmallBlock),
                        worker_lds(c->nb), w.stream, W);
     YRSS_HIP(hipGetLastError());
@@ -3366,11 +3400,16 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
     const uint64_t life_ms = el ? strtoull(el, nullptr, 10) : 1000u;
     w.idle_ticks = std::min<uint64_t>(idle_ms, 10000u) * (uint64_t)khz;
     w.life_ticks = std::min<uint64_t>(std::max<uint64_t>(life_ms, 1u), 10000u) * (uint64_t)khz;
+    if (const char *e = getenv("YRSS_WORKER_POLL_SLEEP"))
+        w.poll_sleep = (uint32_t)std::min(std::max(atoi(e), 1), 256);
     const size_t S = nslots, M = kWorkerMaxBurst;
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipHostMalloc((void **)&w.slots, S * sizeof(WorkerSlot), hipHostMallocCoherent)) !=
             hipSuccess ||
+        (e = hipHostMalloc((void **)&w.done, S * sizeof(uint64_t), hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipMalloc((void **)&w.fault, nblocks * sizeof(uint32_t))) != hipSuccess ||
         (e = hipHostMalloc((void **)&w.next, nblocks * sizeof(uint64_t), hipHostMallocCoherent)) !=
             hipSuccess ||
         (e = hipHostMalloc((void **)&w.ctl, sizeof(WorkerCtl), hipHostMallocCoherent)) !=
@@ -3385,6 +3424,7 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
         (e = hipMalloc((void **)&w.win, (size_t)nblocks * M * YRSS_WIN_FULL)) != hipSuccess ||
         (e = hipMalloc((void **)&w.len, (size_t)nblocks * M * 2u)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_slots, w.slots, 0)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void **)&w.d_done, w.done, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_next, w.next, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_ctl, w.ctl, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&w.d_ptrs, w.ptrs, 0)) != hipSuccess ||
@@ -3397,12 +3437,13 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
         return hip_fail("yrss_worker_start", e);
     }
     memset((void *)w.slots, 0, S * sizeof(WorkerSlot));
+    memset((void *)w.done, 0, S * sizeof(uint64_t));
     for (uint32_t b = 0; b < nblocks; ++b)
         w.next[b] = b + 1u;            // tickets start at 1; block b serves b+1, b+1+B, ...
     memset((void *)w.ctl, 0, sizeof(WorkerCtl));
     w.out = new yrss_ctx::WorkerState::Out[S];
     for (size_t i = 0; i < S; ++i)
-        w.out[i] = yrss_ctx::WorkerState::Out{nullptr, nullptr, nullptr, nullptr, 0u, true};
+        w.out[i] = yrss_ctx::WorkerState::Out{nullptr, nullptr, nullptr, nullptr, 0u, true, 0u};
     w.issued = 0;
     w.on = true;
     return 0;
@@ -3429,16 +3470,42 @@ int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t 
     memcpy(w.ptrs + (size_t)si * kWorkerMaxBurst, ptrs, (size_t)n * 8u);
     if (lens)
         memcpy(w.lens + (size_t)si * kWorkerMaxBurst, lens, (size_t)n * 2u);
+    // Outputs the caller keeps in registered memory are written there by the
+    // GPU (the poll copies nothing); others go through the slot's staging.
+    const size_t base = (size_t)si * kWorkerMaxBurst;
+    void *const user[4] = {out_q, out_hash, out_qidx, out_qstart};
+    const size_t bytes[4] = {(size_t)n * 2u, (size_t)n * 4u, (size_t)n * 4u,
+                             (c->nb + 1u) * 4u};
+    void *const stage[4] = {w.d_q + base, w.d_hash + base, w.d_qidx + base,
+                            w.d_qstart + (size_t)si * w.qs_stride};
+    uint8_t copy = 0;
+    for (int k = 0; k < 4; ++k) {
+        uint64_t d = 0;
+        if (user[k]) {
+            const uint64_t u = (uint64_t)(uintptr_t)user[k];
+            for (uint32_t r = 0; r < c->nranges && !d; ++r)
+                if (u >= c->ranges[r].lo && u + bytes[k] <= c->ranges[r].hi)
+                    d = u + (uint64_t)c->ranges[r].delta;
+            if (!d) {
+                d = (uint64_t)(uintptr_t)stage[k];
+                copy |= (uint8_t)(1u << k);
+            }
+        }
+        sl->out[k] = d;
+    }
     sl->n = n;
     sl->flags = flags;
-    w.out[si] = yrss_ctx::WorkerState::Out{out_q, out_hash, out_qidx, out_qstart, n, false};
+    w.out[si] = yrss_ctx::WorkerState::Out{out_q, out_hash, out_qidx, out_qstart, n, false, copy};
+    ++w.pending;
     __atomic_store_n(&sl->seq, t, __ATOMIC_RELEASE);   // n and flags become visible first
     __atomic_store_n(&w.ctl->pub, t, __ATOMIC_RELAXED);  // ring activity (idle is collective)
     w.issued = t;
     *ticket = t;
     const int rc = worker_ensure(c);   // one cached load unless a workgroup left
-    if (rc)
+    if (rc) {
         w.out[si].collected = true;    // no launch serves it: the slot is free again
+        --w.pending;
+    }
     return rc;
 }
 
@@ -3472,12 +3539,13 @@ int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
         return -EINVAL;
     auto &w = c->w;
     const uint32_t si = (uint32_t)(ticket % w.nslots);
-    WorkerSlot *sl = w.slots + si;
+    const uint64_t *dn = w.done + si;
     auto &o = w.out[si];
     if (ticket + w.nslots <= w.issued || o.collected)
         return -EINVAL;   // reused or already collected
     uint64_t spins = 0, t0 = 0;
-    while (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != ticket) {
+    uint64_t d;
+    while (((d = __atomic_load_n(dn, __ATOMIC_ACQUIRE)) & ~kWorkerFault) != ticket) {
         const int rc = worker_ensure(c);   // a launch that left: relaunch
         if (rc)
             return rc;
@@ -3493,15 +3561,17 @@ int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
         __builtin_ia32_pause();
     }
     o.collected = true;
-    if (__atomic_load_n(&sl->fault, __ATOMIC_ACQUIRE))
+    --w.pending;
+    if (d & kWorkerFault)
         return -EFAULT;
     const size_t base = (size_t)si * kWorkerMaxBurst;
-    memcpy(o.q, w.q + base, (size_t)o.n * 2u);
-    if (o.hash)
+    if (o.copy & 1u)
+        memcpy(o.q, w.q + base, (size_t)o.n * 2u);
+    if (o.copy & 2u)
         memcpy(o.hash, w.hash + base, (size_t)o.n * 4u);
-    if (o.qidx)
+    if (o.copy & 4u)
         memcpy(o.qidx, w.qidx + base, (size_t)o.n * 4u);
-    if (o.qstart)
+    if (o.copy & 8u)
         memcpy(o.qstart, w.qstart + (size_t)si * w.qs_stride, (c->nb + 1u) * 4u);
     return 0;
 }
