@@ -40,3 +40,27 @@ def test_registered_dispatcher_matches_oracle(dev, oracle_mod, cfg):
     # yrss_fini cleared the context it owned: back to the error value
     buf = ctypes.create_string_buffer(frames[0], len(frames[0]))
     assert fn(ctypes.cast(buf, ctypes.c_void_p), len(frames[0]), 0, cfg[1]) == -1
+
+
+def test_python_wrappers(dev, oracle_mod):
+    """SoftRss.toeplitz_dispatch and SoftRss.worker_submit_frames."""
+    cfg = (3, 3, 1, 1)
+    frames = _frames(oracle_mod, 200, 606)
+    q, h, _, _ = _expect(oracle_mod, frames, cfg)
+    from test_gpu_parity import _fake_mbufs
+    pool, ptrs, _ = _fake_mbufs(frames, headroom=128)
+    data = (ptrs + np.uint64(128 + 128)).astype(np.uint64)
+    lens = np.array([len(f) for f in frames], np.uint16)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        assert [eng.toeplitz_dispatch(f) for f in frames[:40]] == [int(x) for x in q[:40]]
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(4, 2)
+        tks = [eng.worker_submit_frames(data[i:i + 50], lens[i:i + 50]) for i in (0, 50, 100, 150)]
+        for k, t in enumerate(tks):
+            r = eng.worker_poll(t)
+            sl = slice(50 * k, 50 * k + 50)
+            qi, qs = oracle_mod.process_burst(q[sl], cfg[1])
+            assert np.array_equal(r.q, q[sl]) and np.array_equal(r.hash, h[sl])
+            assert np.array_equal(r.qidx, qi) and np.array_equal(r.qstart[: qs.size], qs)
+        eng.worker_stop()
+        eng.unregister_host_memory(pool.ctypes.data)

@@ -239,6 +239,36 @@ class SoftRss:
                                            None if qi is None else qi[:n], qs)
         return t.value
 
+    def worker_submit_frames(self, data_ptrs: np.ndarray, lens: np.ndarray, want_hash=True,
+                             compact=True) -> int:
+        """Queue one burst of (frame data pointer, data_len) pairs in registered
+        memory (``yrss_worker_submit_frames``); returns its ticket."""
+        dp = np.ascontiguousarray(data_ptrs, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint16)
+        n = int(dp.size)
+        if ln.size != n:
+            raise ValueError("data_ptrs and lens differ in length")
+        q = np.empty(max(n, 1), np.int16)
+        h = np.empty(max(n, 1), np.uint32) if want_hash else None
+        qi = np.empty(max(n, 1), np.uint32) if compact else None
+        qs = np.empty(self.nb_queues + 2, np.uint32) if compact else None
+        t = ctypes.c_uint64()
+        rc = self._lib.yrss_worker_submit_frames(self._ctx, _ptr(dp), _ptr(ln), n, _ptr(q),
+                                                 _ptr(h), _ptr(qi), _ptr(qs), ctypes.byref(t))
+        abi.check(rc, "yrss_worker_submit_frames")
+        self._wk[t.value] = DispatchResult(q[:n], None if h is None else h[:n],
+                                           None if qi is None else qi[:n], qs)
+        return t.value
+
+    def toeplitz_dispatch(self, frame: bytes, queue_id: int = 0) -> int:
+        """The per-packet registration shim (``yrss_toeplitz_dispatch``) on this
+        context: ``toeplitz_dispatch``'s return value for one frame, computed on
+        the GPU.  One launch per call: for compatibility, not speed."""
+        abi.check(self._lib.yrss_set_dispatch_ctx(self._ctx), "yrss_set_dispatch_ctx")
+        buf = ctypes.create_string_buffer(bytes(frame), len(frame))
+        return int(self._lib.yrss_toeplitz_dispatch(ctypes.cast(buf, ctypes.c_void_p),
+                                                    len(frame), queue_id, self.nb_queues))
+
     def worker_poll(self, ticket: int, wait: bool = True):
         """The burst's DispatchResult, or None while it is pending (wait=False)."""
         rc = self._lib.yrss_worker_poll(self._ctx, ticket, 1 if wait else 0)
