@@ -158,7 +158,7 @@ def test_worker_low_rate_no_stall(dev, oracle_mod, monkeypatch):
     """Fewer than B bursts per idle period: idle is judged over the whole
     ring, so no workgroup leaves while the others keep serving (its tickets
     would wait for the rest of the launch to go idle)."""
-    monkeypatch.setenv("YRSS_WORKER_IDLE_MS", "5")
+    monkeypatch.setenv("YRSS_WORKER_IDLE_MS", "20")
     cfg = (4, 4, 1, 1)
     nb, per, nburst = 8, 16, 40
     frames = _frames(oracle_mod, per * nburst, 77)
@@ -176,11 +176,12 @@ def test_worker_low_rate_no_stall(dev, oracle_mod, monkeypatch):
             lat.append(time.perf_counter() - t0)
             qi, qs = oracle_mod.process_burst(q[lo:lo + per], cfg[1])
             _check(r, q[lo:lo + per], h[lo:lo + per], qi, qs)
-            time.sleep(0.002)        # each workgroup sees a burst every ~16 ms
+            time.sleep(0.005)        # each workgroup sees a burst every ~40 ms
         eng.worker_stop()
         eng.unregister_host_memory(pool.ctypes.data)
-    # the first burst includes the launch; a stranded ticket would take >= 5 ms
-    assert max(lat[1:]) < 0.003, sorted(lat)[-5:]
+    # the first burst includes the launch; a stranded ticket would wait for the
+    # rest of the launch to idle out (up to 20 ms); a served one takes ~20 us
+    assert max(lat[1:]) < 0.010, sorted(lat)[-5:]
 
 
 def test_worker_relaunch_nonblocking_poll(dev, oracle_mod, monkeypatch):
