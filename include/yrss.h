@@ -346,6 +346,24 @@ int yrss_rss_lport_sweep(yrss_ctx *ctx, uint32_t faddr, uint32_t laddr, uint16_t
                          uint16_t nb_queues, uint16_t reta_size, uint16_t queueid,
                          uint32_t *bitmap);
 
+/* ---- multi-GPU sharding ------------------------------------------ */
+
+/* One yrss_ctx and one stream per GPU; each classifies a contiguous shard of the
+ * batch with no collective.  yrss_shard_range gives shard `rank` of `world`
+ * (balanced: the first n_total % world shards get one packet more).
+ * yrss_merge_queue_lists concatenates the shards' per-queue lists in shard
+ * order, which keeps every queue FIFO over the whole batch, as the reference's
+ * rte_ring does (fs/lib/ff_dpdk_if.c:1087-1093): nbk = nb_queues + 1 buckets;
+ * shard s holds qidx[s] (shard-local indices) and qstart[s] (nbk + 1 offsets)
+ * and starts at global packet first[s]; out_qidx gets global indices (64-bit:
+ * a node's batch can exceed 2^32 packets), out_qstart nbk + 1 offsets.
+ * Host-only.  yastack_amd/shard.py is the Python twin. */
+int yrss_shard_range(uint64_t n_total, uint32_t world, uint32_t rank, uint64_t *first,
+                     uint64_t *count);
+int yrss_merge_queue_lists(uint32_t nshards, uint32_t nbk, const uint64_t *first,
+                           const uint32_t *const *qidx, const uint32_t *const *qstart,
+                           uint64_t *out_qidx, uint64_t *out_qstart);
+
 /* ---- pcap capture I/O ----------------------------------- */
 
 /* ff_enable_pcap + ff_dump_packets (fs/lib/ff_dpdk_pcap.c:49-102) for a burst:

@@ -62,3 +62,40 @@ def test_merge_matches_whole_batch(oracle_mod):
     qi_m, qs_m = merge_queue_lists(parts)
     assert np.array_equal(qs_m, qs_all.astype(np.int64))
     assert np.array_equal(qi_m, qi_all.astype(np.int64))
+
+
+def test_c_shard_helpers_match_python(oracle_mod):
+    """yrss_shard_range / yrss_merge_queue_lists (C ABI, host-only) agree with
+    shard.py and with the whole-batch lists."""
+    import ctypes
+
+    from yastack_amd import abi
+
+    lib = abi.load()
+    f, cnt = ctypes.c_uint64(), ctypes.c_uint64()
+    for n, w in [(0, 1), (10, 3), (1 << 33, 8), (7, 8)]:
+        for r in range(w):
+            assert lib.yrss_shard_range(n, w, r, ctypes.byref(f), ctypes.byref(cnt)) == 0
+            assert (f.value, cnt.value) == shard_range(n, w, r)
+    assert lib.yrss_shard_range(5, 2, 2, ctypes.byref(f), ctypes.byref(cnt)) == -22
+
+    win, lens = oracle_mod.synth(6, 5000, stride=80)
+    c = oracle_mod.cfg(5, 4, 1, 0)
+    q, _ = oracle_mod.dispatch_windows(win, 80, lens, c)
+    qi_all, qs_all = oracle_mod.process_burst(q, 4)
+    shards = [shard_range(5000, 4, r) for r in range(4)]
+    parts = [oracle_mod.process_burst(q[a:a + k], 4) for a, k in shards]
+    qis = [np.ascontiguousarray(p[0], np.uint32) for p in parts]
+    qss = [np.ascontiguousarray(p[1], np.uint32) for p in parts]
+    first = np.array([a for a, _ in shards], np.uint64)
+    qi_ptrs = (ctypes.c_void_p * 4)(*[x.ctypes.data for x in qis])
+    qs_ptrs = (ctypes.c_void_p * 4)(*[x.ctypes.data for x in qss])
+    out_qi = np.zeros(5000, np.uint64)
+    out_qs = np.zeros(6, np.uint64)
+    assert lib.yrss_merge_queue_lists(4, 5, first.ctypes.data, ctypes.cast(qi_ptrs, ctypes.c_void_p),
+                                      ctypes.cast(qs_ptrs, ctypes.c_void_p), out_qi.ctypes.data,
+                                      out_qs.ctypes.data) == 0
+    assert np.array_equal(out_qs, qs_all.astype(np.uint64))
+    assert np.array_equal(out_qi, qi_all.astype(np.uint64))
+    qi_py, qs_py = merge_queue_lists([(a, p[0], p[1]) for (a, _), p in zip(shards, parts)])
+    assert np.array_equal(out_qi.astype(np.int64), qi_py)

@@ -158,6 +158,10 @@ _PROTOS = {
     "yrss_worker_stop": (ctypes.c_int, [_vp]),
     "yrss_dispatch_frames_zc_ex": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp,
                                                   _u32]),
+    "yrss_shard_range": (ctypes.c_int, [ctypes.c_uint64, _u32, _u32,
+                                        ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.POINTER(ctypes.c_uint64)]),
+    "yrss_merge_queue_lists": (ctypes.c_int, [_u32, _u32, _vp, _vp, _vp, _vp, _vp]),
     "yrss_set_dispatch_ctx": (ctypes.c_int, [_vp]),
     "yrss_toeplitz_dispatch": (ctypes.c_int, [_vp, ctypes.c_uint16, ctypes.c_uint16,
                                               ctypes.c_uint16]),
