@@ -296,3 +296,58 @@ def test_worker_direct_outputs(dev, oracle_mod):
         eng.worker_stop()
         eng.unregister_host_memory(arena.ctypes.data)
         eng.unregister_host_memory(pool.ctypes.data)
+
+
+@pytest.mark.parametrize("registered", [True, False])
+def test_worker_per_slot_outputs(dev, oracle_mod, registered):
+    """F-Stack's pattern: one fixed set of output arrays per ring slot, reused
+    burst after burst (the workgroups then keep the slot's output addresses and
+    skip reading them).  Sizes vary, so stale addresses or counts would show."""
+    cfg = (6, 5, 1, 1)
+    nslots, nblocks = 8, 2
+    rng = np.random.default_rng(5)
+    sizes = [int(x) for x in rng.integers(1, 300, 48)]
+    frames = _frames(oracle_mod, sum(sizes), 88)
+    pool, ptrs, _ = _fake_mbufs(frames)
+    q_all, h_all, _, _ = _expect(oracle_mod, frames, cfg)
+    lib = abi.load()
+    arena = np.zeros(nslots * 4096, np.uint8)
+    outs = []
+    for k in range(nslots):
+        base = arena[k * 4096:(k + 1) * 4096]
+        if registered:
+            outs.append((base[0:600].view(np.int16), base[640:1840].view(np.uint32),
+                         base[1856:3056].view(np.uint32), base[3072:3072 + 4 * 8].view(np.uint32)))
+        else:
+            outs.append((np.zeros(300, np.int16), np.zeros(300, np.uint32),
+                         np.zeros(300, np.uint32), np.zeros(8, np.uint32)))
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.register_host_memory(arena.ctypes.data, arena.nbytes)
+        eng.worker_start(nslots, nblocks)
+        off, pend = 0, []
+        for i, n in enumerate(sizes):
+            if len(pend) == nslots:
+                _check_slot(lib, eng, oracle_mod, pend.pop(0), q_all, h_all, cfg)
+            q, h, qi, qs = outs[i % nslots]
+            t = ctypes.c_uint64()
+            mb = np.ascontiguousarray(ptrs[off:off + n])
+            assert lib.yrss_worker_submit(eng._ctx, mb.ctypes.data, n, q.ctypes.data,
+                                          h.ctypes.data, qi.ctypes.data, qs.ctypes.data, 0,
+                                          ctypes.byref(t)) == 0
+            pend.append((t.value, off, n, outs[i % nslots]))
+            off += n
+        while pend:
+            _check_slot(lib, eng, oracle_mod, pend.pop(0), q_all, h_all, cfg)
+        eng.worker_stop()
+        eng.unregister_host_memory(arena.ctypes.data)
+        eng.unregister_host_memory(pool.ctypes.data)
+
+
+def _check_slot(lib, eng, oracle_mod, item, q_all, h_all, cfg):
+    t, o, n, (q, h, qi, qs) = item
+    assert lib.yrss_worker_poll(eng._ctx, t, 1) == 0
+    qr = q_all[o:o + n]
+    qi_ref, qs_ref = oracle_mod.process_burst(qr, cfg[1])
+    assert np.array_equal(q[:n], qr) and np.array_equal(h[:n], h_all[o:o + n]), t
+    assert np.array_equal(qi[:n], qi_ref) and np.array_equal(qs[: qs_ref.size], qs_ref), t

@@ -61,6 +61,8 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
     const int frames = fe && atoi(fe) != 0;
     if (frames)
         fill_frames(mbufs, pool, fdata, flen);   /* outside the timed region */
+    const char *so = getenv("YRSS_CBENCH_WORKER_SLOTOUT");
+    const int slotout = so && atoi(so) != 0;
     const char *de = getenv("YRSS_CBENCH_WORKER_DEPTH");
     const char *be = getenv("YRSS_CBENCH_WORKER_BLOCKS");
     unsigned blocks = be ? (unsigned)atoi(be) : 4u;
@@ -103,10 +105,13 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
                 return 3;
             }
             const uint64_t c1 = __rdtsc();
-            rc = frames ? yrss_worker_submit_frames(ctx, fdata + off, flen + off, B, q_all + off,
-                                                    h_all + off, qi_all + off, qs[k], &tk[k])
-                        : yrss_worker_submit(ctx, mbufs + off, B, q_all + off, h_all + off,
-                                             qi_all + off, qs[k], 0, &tk[k]);
+            /* YRSS_CBENCH_WORKER_SLOTOUT=1: one fixed output set per ring slot (the
+             * F-Stack pattern), else outputs follow the packets through the arena */
+            const size_t oo = slotout ? (size_t)k * B : off;
+            rc = frames ? yrss_worker_submit_frames(ctx, fdata + off, flen + off, B, q_all + oo,
+                                                    h_all + oo, qi_all + oo, qs[k], &tk[k])
+                        : yrss_worker_submit(ctx, mbufs + off, B, q_all + oo, h_all + oo,
+                                             qi_all + oo, qs[k], 0, &tk[k]);
             cyc_poll += c1 - c0;
             cyc_sub += __rdtsc() - c1;
             ++nb;

@@ -1519,6 +1519,10 @@ struct alignas(64) WorkerSlot {
 // Consecutive slots share a line, so a host polling in ticket order misses
 // once per eight bursts instead of once per burst.
 constexpr uint64_t kWorkerFault = 1ull << 63;
+// flags bit: the slot's output addresses equal those of its previous burst, so
+// a workgroup that cached them may skip reading them (one PCIe round trip)
+constexpr uint32_t kWorkerSameOut = 1u << 17;
+constexpr uint32_t kWorkerOutCache = 32;   // cached slots per workgroup (LDS)
 constexpr uint32_t kWorkerFrames = 1u << 16;   // slot holds (data, data_len) pairs
 static_assert(sizeof(WorkerSlot) == 64, "one line per slot header");
 
@@ -1552,7 +1556,12 @@ struct WorkerParams {
     uint32_t poll_sleep; // s_sleep(2) units between two polls of a slot
 };
 
-size_t worker_lds(uint32_t nb) { return small_lds(nb, false) + 64u; }
+// small_burst_body's LDS, then 64 B of control words, then the output-address
+// cache: kWorkerOutCache slots x 4 addresses and one valid word per slot
+size_t worker_lds(uint32_t nb)
+{
+    return small_lds(nb, false) + 64u + kWorkerOutCache * (32u + 4u);
+}
 
 __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
 {
@@ -1561,6 +1570,13 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
     const uint32_t lane = lane_id();
     const SmallLds L = small_carve(smem, wave, W.P.nb);
     uint32_t *ctl = reinterpret_cast<uint32_t *>(smem + small_lds(W.P.nb, false));
+    uint64_t *ocache = reinterpret_cast<uint64_t *>(ctl + 16);
+    uint32_t *ovalid = reinterpret_cast<uint32_t *>(ocache + 4 * kWorkerOutCache);
+    // slots of this workgroup: slot of ticket t is t mod nslots, and the
+    // workgroup's tickets are b+1 + kB, so its slots are (b+1 + kB) mod nslots
+    const uint32_t my_slots = W.nslots / gridDim.x;
+    for (uint32_t i = threadIdx.x; i < kWorkerOutCache; i += blockDim.x)
+        ovalid[i] = 0u;
     small_tables<false>(W.P, L);
 
     uint64_t t = __hip_atomic_load(W.next + blockIdx.x, __ATOMIC_RELAXED,
@@ -1615,11 +1631,26 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 __hip_atomic_store(W.fault + blockIdx.x, 0u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
+                // local index of this slot among the workgroup's slots
+                const uint32_t li = si / gridDim.x;
+                const bool cacheable = my_slots <= kWorkerOutCache;
                 uint64_t o[4];
+                if (cacheable && (ctl[2] & kWorkerSameOut) && ovalid[li]) {
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    o[k] = __hip_atomic_load(&sl->out[k], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_SYSTEM);
+                    for (int k = 0; k < 4; ++k)
+                        o[k] = ocache[4 * li + k];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        o[k] = __hip_atomic_load(&sl->out[k], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (cacheable) {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k)
+                            ocache[4 * li + k] = o[k];
+                        ovalid[li] = 1u;
+                    }
+                }
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     ctl[4 + 2 * k] = (uint32_t)o[k];
@@ -1845,6 +1876,7 @@ struct yrss_ctx {
         uint16_t *len = nullptr;
         uint64_t issued = 0;       // last ticket handed out
         uint32_t pending = 0;      // submitted, not yet polled
+        uint64_t *last_out = nullptr;   // [nslots][4] output addresses of each slot's last burst
         struct Out {
             int16_t *q;
             uint32_t *hash, *qidx, *qstart;
@@ -3305,6 +3337,7 @@ void worker_free(yrss_ctx *c)
     if (w.stream)
         (void)hipStreamDestroy(w.stream);
     delete[] w.out;
+    delete[] w.last_out;
     w = yrss_ctx::WorkerState{};
 }
 
@@ -3442,6 +3475,10 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
         w.next[b] = b + 1u;            // tickets start at 1; block b serves b+1, b+1+B, ...
     memset((void *)w.ctl, 0, sizeof(WorkerCtl));
     w.out = new yrss_ctx::WorkerState::Out[S];
+    w.last_out = new uint64_t[4 * S];
+    for (size_t i = 0; i < 4 * S; ++i)
+        w.last_out[i] = ~0ull;   // no previous burst: never "same"
+
     for (size_t i = 0; i < S; ++i)
         w.out[i] = yrss_ctx::WorkerState::Out{nullptr, nullptr, nullptr, nullptr, 0u, true, 0u};
     w.issued = 0;
@@ -3479,6 +3516,7 @@ int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t 
     void *const stage[4] = {w.d_q + base, w.d_hash + base, w.d_qidx + base,
                             w.d_qstart + (size_t)si * w.qs_stride};
     uint8_t copy = 0;
+    bool same = w.last_out != nullptr;
     for (int k = 0; k < 4; ++k) {
         uint64_t d = 0;
         if (user[k]) {
@@ -3492,9 +3530,13 @@ int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t 
             }
         }
         sl->out[k] = d;
+        if (same && w.last_out[4 * si + k] != d)
+            same = false;
+        if (w.last_out)
+            w.last_out[4 * si + k] = d;
     }
     sl->n = n;
-    sl->flags = flags;
+    sl->flags = flags | (same ? kWorkerSameOut : 0u);
     w.out[si] = yrss_ctx::WorkerState::Out{out_q, out_hash, out_qidx, out_qstart, n, false, copy};
     ++w.pending;
     __atomic_store_n(&sl->seq, t, __ATOMIC_RELEASE);   // n and flags become visible first
@@ -3505,6 +3547,8 @@ int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t 
     if (rc) {
         w.out[si].collected = true;    // no launch serves it: the slot is free again
         --w.pending;
+        for (int k = 0; k < 4; ++k)    // and no workgroup cached its addresses
+            w.last_out[4 * si + k] = ~0ull;
     }
     return rc;
 }
