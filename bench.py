@@ -226,15 +226,17 @@ def pcie_inclusive(profile: str):
                 continue
             out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
                         "mpps": d["mpps"], "note": d.get("note", "")})
-    # persistent worker: 128 workgroups, 512 bursts in flight, bursts of 32 and 1024,
-    # mbuf pointers and (data, data_len) pairs, one output set per ring slot
-    for frames in ("0", "1"):
+    # persistent worker, mbuf pointers and (data, data_len) pairs, one output set
+    # per ring slot: 32-packet bursts on 128 workgroups, 1024-packet bursts on 32
+    # (the best counts of the sweeps), ring depth 4 x workgroups
+    for frames, burst, blocks in (("0", 32, 128), ("0", 1024, 32), ("1", 32, 128),
+                                  ("1", 1024, 32)):
         try:
-            r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), "0", "1"],
+            r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
                                env={**os.environ, "YRSS_CBENCH_MODES": "4",
-                                    "YRSS_CBENCH_WORKER_DEPTH": "512",
-                                    "YRSS_CBENCH_WORKER_BLOCKS": "128",
+                                    "YRSS_CBENCH_WORKER_DEPTH": str(4 * blocks),
+                                    "YRSS_CBENCH_WORKER_BLOCKS": str(blocks),
                                     "YRSS_CBENCH_WORKER_SLOTOUT": "1",
                                     "YRSS_CBENCH_WORKER_FRAMES": frames})
         except subprocess.TimeoutExpired:
