@@ -49,7 +49,7 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--profile", default="udp4", choices=sorted(PROFILES))
     ap.add_argument("--pkts", type=int, default=1 << 24, help="packets per GPU")
     ap.add_argument("--stride", type=int, default=64)
