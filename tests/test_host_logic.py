@@ -99,3 +99,33 @@ def test_c_shard_helpers_match_python(oracle_mod):
     assert np.array_equal(out_qi, qi_all.astype(np.uint64))
     qi_py, qs_py = merge_queue_lists([(a, p[0], p[1]) for (a, _), p in zip(shards, parts)])
     assert np.array_equal(out_qi.astype(np.int64), qi_py)
+
+
+def test_dispatch_dev_refuses_short_buffers():
+    """The Python device-path wrapper checks buffer sizes before the raw
+    pointers reach the GPU (a short buffer would fault the device)."""
+    from yastack_amd.dispatch import DispatchResult, _check_dev_sizes
+
+    class T:   # minimal tensor stand-in: numel / element_size
+        def __init__(self, n, es):
+            self.n, self.es = n, es
+
+        def numel(self):
+            return self.n
+
+        def element_size(self):
+            return self.es
+
+    out = DispatchResult(T(100, 2), T(100, 4), T(100, 4), T(5, 4))
+    _check_dev_sizes(100, 64, T(6400, 1), T(100, 2), out, 3)
+    _check_dev_sizes(0, 64, T(64, 1), T(1, 2), out, 3)
+    for bad in [dict(win=T(6399, 1)), dict(lens=T(99, 2))]:
+        args = dict(win=T(6400, 1), lens=T(100, 2))
+        args.update(bad)
+        with pytest.raises(ValueError):
+            _check_dev_sizes(100, 64, args["win"], args["lens"], out, 3)
+    with pytest.raises(ValueError):
+        _check_dev_sizes(101, 64, T(6464, 1), T(101, 2), out, 3)      # outputs too short
+    with pytest.raises(ValueError):
+        _check_dev_sizes(100, 64, T(6400, 1), T(100, 2),
+                         DispatchResult(T(100, 2), T(100, 4), T(100, 4), T(3, 4)), 3)

@@ -48,6 +48,31 @@ class DispatchResult:
         return self.qidx[int(s[b]):int(s[b + 1])]
 
 
+def _check_dev_sizes(n, stride, win, lens, out, nb_queues):
+    """The C ABI takes raw device pointers and cannot see the buffers' sizes: a
+    batch larger than its buffers would fault the GPU.  Refuse it here."""
+    def nbytes(t):
+        return 0 if t is None else int(t.numel()) * int(t.element_size())
+    if n < 0:
+        raise ValueError("negative batch size")
+    if n == 0:
+        return
+    # the kernel may read any byte below the stride of a window (rare header walks)
+    need = [("win", win, n * stride), ("lens", lens, 2 * n),
+            ("q", out.q, 2 * n)]
+    if out.hash is not None:
+        need.append(("hash", out.hash, 4 * n))
+    if out.qidx is not None:
+        need.append(("qidx", out.qidx, 4 * n))
+    if out.qstart is not None:
+        need.append(("qstart", out.qstart, 4 * (nb_queues + 1)))
+    if out.filter is not None:
+        need.append(("filter", out.filter, n))
+    for name, t, b in need:
+        if nbytes(t) < b:
+            raise ValueError(f"{name} holds {nbytes(t)} bytes, the batch of {n} needs {b}")
+
+
 def _ptr(t) -> int | None:
     if t is None:
         return None
@@ -139,6 +164,7 @@ class SoftRss:
         dev = lens.device
         if out is None:
             out = self.alloc_out(n, dev, want_hash, compact, want_filter)
+        _check_dev_sizes(n, stride, win, lens, out, self.nb_queues)
         b = abi.DevBatch(_ptr(win), stride, n, _ptr(lens), _ptr(out.q), _ptr(out.hash),
                          _ptr(out.qidx), _ptr(out.qstart), _ptr(out.filter))
         rc = self._lib.yrss_dispatch_dev_ex(self._ctx, ctypes.byref(b), self._stream(stream))
