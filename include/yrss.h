@@ -145,6 +145,9 @@ void yrss_fini(yrss_ctx *ctx);
  *              d_qstart[b+1]).  d_qstart[nb_queues+1] == n.
  *   stream     hipStream_t (NULL = legacy default stream)
  * n <= YRSS_MAX_BATCH.  Asynchronous: returns after enqueueing the kernels.
+ * Batches of <= 4096 packets (with nb_queues + 1 <= 64) run as one launch of
+ * the one-workgroup burst kernel instead of parse + scan + scatter (same
+ * outputs; yrss_timing_* does not count it; YRSS_SMALL_DEV=0 turns it off).
  * Dispatches of one context share its compaction workspace: a dispatch on a
  * different stream than the context's previous one waits (on the device) for
  * the work already queued there, so streams may be mixed freely; dispatches

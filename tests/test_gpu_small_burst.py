@@ -238,3 +238,31 @@ def test_async_python_wrapper(dev, oracle_mod):
         _check(r0, *want[0])
         _check(r1, *want[1])
         e1.unregister_host_memory(pool.ctypes.data)
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 1000, 4096, 4097])
+@pytest.mark.parametrize("stride", [64, 80, 2176])
+def test_device_batch_small_path(dev, oracle_mod, monkeypatch, n, stride):
+    """yrss_dispatch_dev batches of <= 4096 packets take the one-launch kernel;
+    outputs (q, hash, filter class, lists) equal the three-kernel path's and
+    the oracle's."""
+    cfg = (5, 4, 1, 1)
+    outs = []
+    for small in ("1", "0"):
+        monkeypatch.setenv("YRSS_SMALL_DEV", small)
+        with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            eng.set_kni(True, "reject", "80,443", "53")
+            win, lens = eng.synth(abi.SYN_FUZZ, n, 77, stride=stride)
+            r = eng.dispatch_dev(win, lens, stride, n, want_filter=True)
+            torch.cuda.synchronize()
+            assert eng.status() == 0
+            outs.append([x[: (n if x.numel() >= n else x.numel())].cpu().numpy()
+                         for x in (r.q, r.hash, r.qidx, r.qstart, r.filter)])
+            w_h = win[: n * stride].cpu().numpy()
+            l_h = lens[:n].cpu().numpy().view(np.uint16)
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    c = oracle_mod.cfg(*cfg)
+    q_ref, h_ref = oracle_mod.dispatch_windows(w_h, stride, l_h, c)
+    assert np.array_equal(outs[0][0].view(np.int16), q_ref)
+    assert np.array_equal(outs[0][1].view(np.uint32), h_ref)

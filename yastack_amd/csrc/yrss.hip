@@ -1843,6 +1843,7 @@ struct yrss_ctx {
     // device views of the pinned staging: the small-burst kernel reads and
     // writes it in place (no copies)
     bool no_small = false;          // YRSS_NO_SMALL: always the multi-kernel path
+    bool small_dev = true;          // YRSS_SMALL_DEV=0: device batches never take it
     uint8_t *dh_win = nullptr;
     uint16_t *dh_len = nullptr;
     int16_t *dh_q = nullptr;
@@ -2214,7 +2215,11 @@ bool small_ok(const yrss_ctx *c, uint32_t n)
 
 // One launch of yrss_burst_small on the context stream.  S.P.win/len and the
 // output pointers are filled by the caller; this adds the configuration.
-int small_launch(yrss_ctx *c, SmallParams &S, bool filter)
+// host_burst: a host-resident burst on the context stream, completed by the
+// host spinning on the kernel's completion word; otherwise a device batch on
+// the caller's stream (no completion word).
+int small_launch(yrss_ctx *c, SmallParams &S, bool filter, bool host_burst = true,
+                 hipStream_t stream = nullptr)
 {
     const ParseParams &proto = c->proto;
     ParseParams &P = S.P;
@@ -2228,15 +2233,20 @@ int small_launch(yrss_ctx *c, SmallParams &S, bool filter)
     P.rank = nullptr;
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
-    S.done = c->spin_wait ? c->dh_done : nullptr;
-    S.seq = ++c->done_seq;
-    c->pend.done_seq = c->spin_wait ? S.seq : 0u;   // the caller reset pend before
+    if (host_burst) {
+        S.done = c->spin_wait ? c->dh_done : nullptr;
+        S.seq = ++c->done_seq;
+        c->pend.done_seq = c->spin_wait ? S.seq : 0u;   // the caller reset pend before
+        stream = c->stream;
+    } else {
+        S.done = nullptr;
+    }
     const size_t lds = small_lds(c->nb, filter);
     const dim3 grid(1);
     if (filter)
-        hipLaunchKernelGGL(yrss_burst_small<true>, grid, dim3(kSmallBlock), lds, c->stream, S);
+        hipLaunchKernelGGL(yrss_burst_small<true>, grid, dim3(kSmallBlock), lds, stream, S);
     else
-        hipLaunchKernelGGL(yrss_burst_small<false>, grid, dim3(kSmallBlock), lds, c->stream, S);
+        hipLaunchKernelGGL(yrss_burst_small<false>, grid, dim3(kSmallBlock), lds, stream, S);
     YRSS_HIP(hipGetLastError());
     return 0;
 }
@@ -2512,6 +2522,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         c->proto.out16 = (uint32_t)std::min(2, std::max(0, atoi(e)));
     if (const char *e = getenv("YRSS_NO_SMALL"))
         c->no_small = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_SMALL_DEV"))
+        c->small_dev = atoi(e) != 0;
     if (const char *e = getenv("YRSS_SPIN_WAIT"))   // A/B: spin vs stream sync
         c->spin_wait = atoi(e) != 0;
     if (const char *e = getenv("YRSS_EVENT_FLAGS"))   // A/B of the timing-event fence
@@ -2687,6 +2699,24 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     }
     c->last_stream = s;
     c->last_stream_valid = true;
+    // Up to 4096 packets: one launch of the one-workgroup burst kernel (parse,
+    // lists in LDS) instead of parse + scan + scatter, ~10 us less per call
+    // (profiles/r01_v26_small_kernel_stats.csv: three launches cost >= 15 us of
+    // kernel time however small the batch).  Not timed by yrss_timing_*.
+    if (small_ok(c, n) && c->small_dev) {
+        SmallParams S;
+        memset(&S, 0, sizeof(S));
+        S.P.win = b->win;
+        S.P.len = b->len;
+        S.P.stride = win_stride;
+        S.P.n = n;
+        S.P.q = b->q;
+        S.P.hash = b->hash;
+        S.P.filter = b->filter;
+        S.qidx = compact ? b->qidx : nullptr;
+        S.qstart = compact ? b->qstart : nullptr;
+        return small_launch(c, S, filter, false, s);
+    }
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
     // 18..65 buckets (16-tile chunks): the parse kernel also emits each
