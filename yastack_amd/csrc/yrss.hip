@@ -1486,18 +1486,20 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_small(SmallParams S)
 // Persistent burst worker (yrss_worker_*): no launch and no stream
 // synchronisation per burst.  The host writes a burst's mbuf pointers into a
 // slot of a ring in host-coherent pinned memory and publishes its ticket in
-// the slot's seq word; workgroup b of this kernel owns tickets b, b + B,
-// b + 2B, ... (B workgroups; slot = ticket mod nslots, nslots a multiple of
-// B), polls the seq word of its next ticket, runs the burst through
-// small_burst_body() (tables stay in LDS across bursts), writes q / hash /
-// lists into the slot's pinned output area and publishes the ticket in the
-// slot's done word.  Every workgroup leaves when the host sets the stop word,
+// the slot's seq word; workgroup b of this kernel owns tickets b+1, b+1+B,
+// ... (B workgroups; slot = ticket mod nslots, nslots a multiple of B), polls
+// the seq word of its next ticket, runs the burst through small_burst_body()
+// (tables stay in LDS across bursts), writes q / hash / lists to the output
+// addresses the slot names (the caller's registered arrays or the slot's
+// pinned staging) and publishes the ticket in done[slot], a separate
+// GPU-written array.  Every workgroup leaves when the host sets the stop word,
 // after the whole ring saw no submit for idle_ticks, or after life_ticks in
 // total, storing the ticket it would have served next and counting itself in
 // WorkerCtl::exited; the host's next submit or poll then stops the rest of
 // the launch and relaunches.
 // Protocol (host-coherent memory, system scope): the host writes ptrs / n /
-// flags, then seq with release; the GPU polls seq relaxed, then acquires.
+// flags / output addresses, then seq with release; the GPU polls seq relaxed,
+// then acquires and reads the addresses (unless its LDS cache has them).
 // The GPU drains every wave's output stores (vmcnt(0) + barrier), releases
 // at system scope, then writes done; the host reads done with acquire.
 // ---------------------------------------------------------------------------
