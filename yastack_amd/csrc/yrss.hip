@@ -184,6 +184,28 @@ __device__ __forceinline__ uint32_t win_byte(const ParseParams &P, const uint32_
 }
 
 // FilterReturn values (ff_dpdk_kni.h:34-38) plus the two boundary outcomes.
+// Toeplitz over one 32-bit tuple word (bit 31-k selects key window k), the two
+// ways: four lookups into byte tables tb[j*256+v] (v = byte j of the word from
+// the top), or bit-serial on the VALU with the windows in SGPRs.
+__device__ __forceinline__ uint32_t tz_lds(uint32_t w, const uint32_t *tb)
+{
+    return tb[w >> 24] ^ tb[256 + ((w >> 16) & 0xffu)] ^ tb[512 + ((w >> 8) & 0xffu)] ^
+           tb[768 + (w & 0xffu)];
+}
+
+__device__ __forceinline__ uint32_t tz_valu(uint32_t w, const uint32_t *kw, uint32_t h)
+{
+#pragma unroll
+    for (int k = 0; k < 32; ++k)   // h ^= (bit ? ~0 : 0) & kw[k]  (truth table 0x6a)
+        h = __builtin_amdgcn_bitop3_b32((uint32_t)((int32_t)(w << k) >> 31), kw[k], h, 0x6a);
+    return h;
+}
+
+#ifndef YRSS_VALU_WORDS
+#define YRSS_VALU_WORDS 0
+#endif
+constexpr int kVw = YRSS_VALU_WORDS;   // tuple words hashed on the VALU (0..3)
+
 constexpr int kFilterUnknown = -1, kFilterArp = 1, kFilterKni = 2;
 constexpr int kFilterTrunc = -2;   // header walk left the staged window
 constexpr int kFilterLoop = -3;    // IPIP with IHL=0: the reference recurses forever
@@ -363,21 +385,26 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
     uint32_t h = 0;
     if (hashed) {
         // Tuple = LE image of ntohl(src), ntohl(dst), ntohs(sport), ntohs(dport)
-        // (ff_dpdk_if.c:1994-2021); 12 byte-table lookups = bit-serial Toeplitz.
-        const uint32_t h_l3 =
-            tbl[0 * 256 + ((d7 >> 8) & 0xffu)] ^     // b29
-            tbl[1 * 256 + (d7 & 0xffu)] ^            // b28
-            tbl[2 * 256 + (d6 >> 24)] ^              // b27
-            tbl[3 * 256 + ((d6 >> 16) & 0xffu)] ^    // b26
-            tbl[4 * 256 + ((d8 >> 8) & 0xffu)] ^     // b33
-            tbl[5 * 256 + (d8 & 0xffu)] ^            // b32
-            tbl[6 * 256 + (d7 >> 24)] ^              // b31
-            tbl[7 * 256 + ((d7 >> 16) & 0xffu)];     // b30
-        h = h_l3 ^
-            tbl[8 * 256 + (pa >> 24)] ^              // b[p+1]
-            tbl[9 * 256 + ((pa >> 16) & 0xffu)] ^    // b[p]
-            tbl[10 * 256 + ((pb >> 8) & 0xffu)] ^    // b[p+3]
-            tbl[11 * 256 + (pb & 0xffu)];            // b[p+2]
+        // (ff_dpdk_if.c:1994-2021).
+        // Tuple words in key order: w0 = saddr, w1 = daddr, w2 = ports; bit 31-k of
+        // wi selects key window 32i+k.  Word i < kVw runs bit-serial on the VALU
+        // (bfe + one 3-input bitop per bit), the rest as 4 byte-table lookups.
+        const uint32_t w0 = __builtin_amdgcn_alignbit(d7, d6, 16);
+        const uint32_t w1 = __builtin_amdgcn_alignbit(d8, d7, 16);
+        uint32_t h_l3 = 0;
+        if (kVw > 0)
+            h_l3 = tz_valu(w0, P.kwin, h_l3);
+        else
+            h_l3 = tz_lds(w0, tbl);
+        if (kVw > 1)
+            h_l3 = tz_valu(w1, P.kwin + 32, h_l3);
+        else
+            h_l3 ^= tz_lds(w1, tbl + 4 * 256);
+        const uint32_t w2 = (pa & 0xffff0000u) | (pb & 0xffffu);
+        if (kVw > 2)
+            h = tz_valu(w2, P.kwin + 64, h_l3);
+        else
+            h = h_l3 ^ tz_lds(w2, tbl + 8 * 256);
         bool trunc = false;
         // Rare slow path, entered only by waves that hold such a packet, so its
         // global loads (and the vmcnt drain they imply) stay off the hot loop.
@@ -387,8 +414,7 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
                     reinterpret_cast<const uint32_t *>(P.win + (size_t)pkt * P.stride);
                 const uint32_t ta = __builtin_nontemporal_load(g + j);
                 const uint32_t tb = __builtin_nontemporal_load(g + j + 1u);
-                h = h_l3 ^ tbl[8 * 256 + (ta >> 24)] ^ tbl[9 * 256 + ((ta >> 16) & 0xffu)] ^
-                    tbl[10 * 256 + ((tb >> 8) & 0xffu)] ^ tbl[11 * 256 + (tb & 0xffu)];
+                h = h_l3 ^ tz_lds((ta & 0xffff0000u) | (tb & 0xffffu), tbl + 8 * 256);
             } else {
                 trunc = true;
             }
