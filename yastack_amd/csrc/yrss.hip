@@ -1812,12 +1812,13 @@ struct yrss_ctx {
     int device = 0;
     int cus = 0;
     // Parse-kernel launch shape (env overrides for tuning sweeps).  Defaults =
-    // best of the on-hardware sweep (profiles/r01_sweep_*.json): non-temporal
-    // window loads are worth ~25 %; 16 waves/CU of 512-thread workgroups keep
-    // ~64 KiB of loads in flight per CU.
+    // best of the on-hardware sweeps (profiles/r01_sweep_*.json,
+    // r01_v30_occupancy_ab.log): non-temporal window loads are worth ~25 %; one
+    // 512-thread workgroup (8 waves) per CU beats 12 or 16 resident waves.
     uint32_t parse_block = 512;  // YRSS_BLOCK: 256 / 512
     bool nt = true;              // YRSS_NT
     uint32_t waves_per_cu = 8;   // YRSS_WAVES_PER_CU: cap on resident waves
+    uint32_t lds_blocks = 0;     // YRSS_LDS_BLOCKS: blocks per CU by LDS (0 = sized for the filter)
     unsigned event_flags = hipEventDisableSystemFence;   // YRSS_EVENT_FLAGS
     uint32_t nb = 0;
     ParseParams proto{};         // key schedule, modulo constants
@@ -1958,7 +1959,8 @@ uint32_t grid_for(const yrss_ctx *c, uint32_t n)
     const uint32_t wpb = c->parse_block / kWave;
     const uint64_t per_block = (uint64_t)wpb * kTile;
     const uint32_t want = (uint32_t)(((uint64_t)n + per_block - 1) / per_block);
-    const uint32_t by_lds = (uint32_t)(160u * 1024u / parse_lds(c, true));
+    const uint32_t by_lds =
+        c->lds_blocks ? c->lds_blocks : (uint32_t)(160u * 1024u / parse_lds(c, true));
     const uint32_t by_waves = std::max(1u, c->waves_per_cu / wpb);
     const uint32_t cap = (uint32_t)c->cus * std::max(1u, std::min(by_lds, by_waves));
     return std::max(1u, std::min(want, cap));
@@ -2544,6 +2546,11 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         const int v = atoi(e);
         if (v >= 4 && v <= kMaxWavesPerCU)
             c->waves_per_cu = (uint32_t)v;
+    }
+    if (const char *e = getenv("YRSS_LDS_BLOCKS")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 8)
+            c->lds_blocks = (uint32_t)v;
     }
     c->proto.out16 = 2;   // 16-byte sc1 bursts (profiles/r01_v13_ahead_out16_ab.log)
     if (const char *e = getenv("YRSS_OUT16"))
