@@ -183,62 +183,15 @@ __device__ __forceinline__ uint32_t win_byte(const ParseParams &P, const uint32_
     return 0u;
 }
 
+// FilterReturn values (ff_dpdk_kni.h:34-38) plus the two boundary outcomes.
 // Toeplitz over one 32-bit tuple word (bit 31-k selects key window k), the two
 // ways: four lookups into byte tables tb[j*256+v] (v = byte j of the word from
 // the top), or bit-serial on the VALU with the windows in SGPRs.
-#ifndef YRSS_SDWA
-#define YRSS_SDWA 0
-#endif
-#if YRSS_SDWA
-// 4 * (byte k of w) in one VALU op (SDWA byte select feeding the shift); the
-// compiler's own form is a bfe and a shift-add per lookup.
-#define YRSS_BYTE_X4(k)                                                                  \
-    __device__ __forceinline__ uint32_t byte_x4_##k(uint32_t w)                          \
-    {                                                                                    \
-        uint32_t r;                                                                      \
-        asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD "          \
-            "src0_sel:DWORD src1_sel:BYTE_" #k                                           \
-            : "=v"(r)                                                                    \
-            : "v"(w));                                                                   \
-        return r;                                                                        \
-    }
-YRSS_BYTE_X4(0)
-YRSS_BYTE_X4(1)
-YRSS_BYTE_X4(2)
-YRSS_BYTE_X4(3)
-#undef YRSS_BYTE_X4
-
-__device__ __forceinline__ uint32_t tz_lds(uint32_t w, const uint32_t *tb)
-{
-    const uint8_t *b = reinterpret_cast<const uint8_t *>(tb);
-    auto at = [b](uint32_t off) { return *reinterpret_cast<const uint32_t *>(b + off); };
-    return at(byte_x4_3(w)) ^ at(1024u + byte_x4_2(w)) ^ at(2048u + byte_x4_1(w)) ^
-           at(3072u + byte_x4_0(w));
-}
-#else
 __device__ __forceinline__ uint32_t tz_lds(uint32_t w, const uint32_t *tb)
 {
     return tb[w >> 24] ^ tb[256 + ((w >> 16) & 0xffu)] ^ tb[512 + ((w >> 8) & 0xffu)] ^
            tb[768 + (w & 0xffu)];
 }
-#endif
-
-#if YRSS_SDWA == 2
-// The byte tables sit at LDS address 0 in every kernel that hashes through
-// process_tile (dynamic LDS, no static __shared__), so table t's entry v is at
-// LDS address t*1024 + 4v and the lookup needs no base add.
-typedef const __attribute__((address_space(3))) uint32_t lds_u32;
-template <uint32_t kBase>
-__device__ __forceinline__ uint32_t tz_lds_abs(uint32_t w)
-{
-    auto at = [](uint32_t off) { return *(lds_u32 *)(uintptr_t)(kBase + off); };
-    return at(byte_x4_3(w)) ^ at(1024u + byte_x4_2(w)) ^ at(2048u + byte_x4_1(w)) ^
-           at(3072u + byte_x4_0(w));
-}
-#define TZ_LDS(w, tb, t) tz_lds_abs<(t) * 1024u>(w)
-#else
-#define TZ_LDS(w, tb, t) tz_lds(w, (tb) + (t) * 256)
-#endif
 
 __device__ __forceinline__ uint32_t tz_valu(uint32_t w, const uint32_t *kw, uint32_t h)
 {
@@ -253,7 +206,6 @@ __device__ __forceinline__ uint32_t tz_valu(uint32_t w, const uint32_t *kw, uint
 #endif
 constexpr int kVw = YRSS_VALU_WORDS;   // tuple words hashed on the VALU (0..3)
 
-// FilterReturn values (ff_dpdk_kni.h:34-38) plus the two boundary outcomes.
 constexpr int kFilterUnknown = -1, kFilterArp = 1, kFilterKni = 2;
 constexpr int kFilterTrunc = -2;   // header walk left the staged window
 constexpr int kFilterLoop = -3;    // IPIP with IHL=0: the reference recurses forever
@@ -443,16 +395,16 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
         if (kVw > 0)
             h_l3 = tz_valu(w0, P.kwin, h_l3);
         else
-            h_l3 = TZ_LDS(w0, tbl, 0);
+            h_l3 = tz_lds(w0, tbl);
         if (kVw > 1)
             h_l3 = tz_valu(w1, P.kwin + 32, h_l3);
         else
-            h_l3 ^= TZ_LDS(w1, tbl, 4);
+            h_l3 ^= tz_lds(w1, tbl + 4 * 256);
         const uint32_t w2 = (pa & 0xffff0000u) | (pb & 0xffffu);
         if (kVw > 2)
             h = tz_valu(w2, P.kwin + 64, h_l3);
         else
-            h = h_l3 ^ TZ_LDS(w2, tbl, 8);
+            h = h_l3 ^ tz_lds(w2, tbl + 8 * 256);
         bool trunc = false;
         // Rare slow path, entered only by waves that hold such a packet, so its
         // global loads (and the vmcnt drain they imply) stay off the hot loop.
@@ -468,20 +420,8 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
             }
         }
         // hash % d exactly (Lemire fastmod, 64-bit M), then +q_off (:2031-2034)
-#if YRSS_MOD_POW2
-        // a power-of-two divisor (the metric config's nb_procs - 1 = 2) is a mask;
-        // the test is uniform, so this is a scalar branch
-        uint32_t rem;
-        if ((P.mod_d & (P.mod_d - 1u)) == 0u) {
-            rem = h & (P.mod_d - 1u);
-        } else {
-            const uint64_t low = P.mod_m * (uint64_t)h;
-            rem = (uint32_t)__umul64hi(low, (uint64_t)P.mod_d);
-        }
-#else
         const uint64_t low = P.mod_m * (uint64_t)h;
         const uint32_t rem = (uint32_t)__umul64hi(low, (uint64_t)P.mod_d);
-#endif
         qv = (int)(uint16_t)(rem + P.q_off);
         if (trunc) {
             qv = YRSS_Q_TRUNCATED;
