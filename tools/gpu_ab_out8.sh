@@ -1,4 +1,5 @@
 # Parse output burst of 8 tiles (YRSS_PARSE_OUT_TILES=8 build, needs 8-tile chunks)
+# Requires the YRSS_PARSE_OUT_TILES build from commit 7115730 (removed from the source afterwards).
 # against the default 4, with 8-tile chunks on the default build as the control.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export PYTHONUNBUFFERED=1

@@ -61,14 +61,6 @@ constexpr int kTblBytes = 12 * 256 * 4;
 constexpr int kRsrcWord3 = 0x00020000;  // buffer resource dword 3 for gfx9-family (CDNA)
 constexpr uint32_t kOutTiles = 4;       // parse: output burst (tiles buffered in LDS)
 constexpr int kOutBytes = kOutTiles * kTile * (4 + 2 + 1 + 2);   // hash, q, filter, rank
-#ifndef YRSS_PARSE_OUT_TILES
-#define YRSS_PARSE_OUT_TILES 4
-#endif
-// parse kernel's own output burst (the small-burst kernels keep kOutTiles)
-constexpr uint32_t kParseOutTiles = YRSS_PARSE_OUT_TILES;
-static_assert(kParseOutTiles == 4 || kParseOutTiles == 8, "parse output burst: 4 or 8 tiles");
-constexpr uint32_t kParseOutLog = kParseOutTiles == 8 ? 3u : 2u;
-constexpr int kParseOutBytes = kParseOutTiles * kTile * (4 + 2 + 1 + 2);
 constexpr int kStageBytes = kTile * 64; // 4 KiB per wave
 
 // Everything yrss_parse_hash needs, passed by value (kernarg segment).
@@ -300,24 +292,18 @@ __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *
         // (sc1: the lines leave L2 at once, none is left dirty at kernel end)
         wave_lds_sync();
         const uint32_t nh = nv >> 2, nq8 = nv >> 3;
-        // out16 == 2 stores write-through (sc1 = 16); 1 plain
-        auto put = [&](const u32x4 &v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
-            if (P.out16 == 2)
-                __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 16);
-            else
-                __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, 0);
-        };
-        for (uint32_t b = 0; b < nh; b += kWave) {
-            const uint32_t l = b + lane;
-            const u32x4 vh = *reinterpret_cast<const u32x4 *>(oh + 4u * min(l, nh - 1u));
-            if (l < nh)
-                put(vh, rh, l * 16u);
-        }
-        for (uint32_t b = 0; b < nq8; b += kWave) {
-            const uint32_t l = b + lane;
-            const u32x4 vq = *reinterpret_cast<const u32x4 *>(oq + 8u * min(l, nq8 - 1u));
-            if (l < nq8)
-                put(vq, rq, l * 16u);
+        const u32x4 vh = *reinterpret_cast<const u32x4 *>(oh + 4u * min(lane, nh - 1u));
+        const u32x4 vq = *reinterpret_cast<const u32x4 *>(oq + 8u * min(lane, nq8 - 1u));
+        if (P.out16 == 2) {
+            if (lane < nh)
+                __builtin_amdgcn_raw_buffer_store_b128(vh, rh, (int)(lane * 16u), 0, 16);
+            if (lane < nq8)
+                __builtin_amdgcn_raw_buffer_store_b128(vq, rq, (int)(lane * 16u), 0, 16);
+        } else {
+            if (lane < nh)
+                __builtin_amdgcn_raw_buffer_store_b128(vh, rh, (int)(lane * 16u), 0, 0);
+            if (lane < nq8)
+                __builtin_amdgcn_raw_buffer_store_b128(vq, rq, (int)(lane * 16u), 0, 0);
         }
         wave_lds_sync();
     } else {
@@ -524,13 +510,13 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     uint32_t *cnt_base =
         reinterpret_cast<uint32_t *>(smem + kTblBytes + kWaves * kStageBytes);
     uint32_t *cnt_w = cnt_base + wave * kCntWords;
-    uint8_t *out_w = reinterpret_cast<uint8_t *>(cnt_base + kWaves * kCntWords) + wave * kParseOutBytes;
+    uint8_t *out_w = reinterpret_cast<uint8_t *>(cnt_base + kWaves * kCntWords) + wave * kOutBytes;
     uint32_t *oh = reinterpret_cast<uint32_t *>(out_w);
-    uint16_t *oq = reinterpret_cast<uint16_t *>(out_w + kParseOutTiles * kTile * 4);
-    int8_t *of = reinterpret_cast<int8_t *>(out_w + kParseOutTiles * kTile * 6);
-    uint16_t *orank = reinterpret_cast<uint16_t *>(out_w + kParseOutTiles * kTile * 7);
+    uint16_t *oq = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 4);
+    int8_t *of = reinterpret_cast<int8_t *>(out_w + kOutTiles * kTile * 6);
+    uint16_t *orank = reinterpret_cast<uint16_t *>(out_w + kOutTiles * kTile * 7);
     uint32_t *kni = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(cnt_base) +
-                                                 kWaves * (kCntWords * 4 + kParseOutBytes));
+                                                 kWaves * (kCntWords * 4 + kOutBytes));
 
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint32_t W = gridDim.x * kWaves;
@@ -576,9 +562,9 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         slot = kk;
         return true;
     };
-    // outputs are buffered per batch of up to kParseOutTiles consecutive tiles of a
+    // outputs are buffered per batch of up to kOutTiles consecutive tiles of a
     // chunk and flushed after its last tile (or the sequence's last)
-    const uint32_t fb_mask = (1u << min(P.ct_shift, kParseOutLog)) - 1u;
+    const uint32_t fb_mask = (1u << min(P.ct_shift, 2u)) - 1u;   // kOutTiles = 4
     auto slot = [&](uint32_t i) {
         const uint32_t j = (i & fb_mask) * kTile;
         return OutSlot{oq + j, oh + j, of + j, orank + j};
@@ -1962,7 +1948,7 @@ int hip_fail(const char *what, hipError_t e)
 size_t parse_lds(const yrss_ctx *c, bool filter)
 {
     const size_t w = c->parse_block / kWave;
-    return kTblBytes + w * kStageBytes + w * (kCntWords * sizeof(uint32_t) + kParseOutBytes) +
+    return kTblBytes + w * kStageBytes + w * (kCntWords * sizeof(uint32_t) + kOutBytes) +
            (filter ? kKniWords * sizeof(uint32_t) : 0u);
 }
 
