@@ -1,3 +1,8 @@
+# A/B of the hash split between LDS byte tables and VALU bit-serial words.
+# Build the variants first, on the CPU side:
+#   for v in 0 1 2 3; do mkdir -p build/vw$v; hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC \
+#     -shared -DYRSS_VALU_WORDS=$v -I include yastack_amd/csrc/yrss.hip yastack_amd/csrc/yrss_pcap.cpp \
+#     yastack_amd/csrc/yrss_shard.cpp -o build/vw$v/libyrss.so; done
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 V="YRSS_LIB=build/vw0/libyrss.so;YRSS_LIB=build/vw1/libyrss.so;YRSS_LIB=build/vw2/libyrss.so;YRSS_LIB=build/vw3/libyrss.so"
