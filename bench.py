@@ -76,14 +76,64 @@ def parse_args(argv=None):
                          "(0: diagnosis only, roofline.achieved is then null)")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_parse_hash.json"),
                     help="rocprofv3 PMC summary used for roofline.traffic")
+    ap.add_argument("--dry", action="store_true",
+                    help="plumbing check without a GPU (rank spawn, barrier, reductions); "
+                         "prints a line marked dry, never a measurement")
     return ap.parse_args(argv)
 
 
 # ---- distributed plumbing (gloo: control only) -----------------------------------
-def dist_setup():
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`python bench.py --gpus N` without a launcher: start N fresh rank
+    processes (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their env) and return
+    the worst exit status.  The parent never touches the GPU: each child picks
+    its device from LOCAL_RANK before any HIP call.  If one rank fails, the
+    others are stopped (they would wait at the barrier)."""
+    import subprocess
+
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = {**os.environ, "RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n),
+               "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": port}
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            s = p.poll()
+            if s is None:
+                continue
+            live.remove(p)
+            if s != 0:
+                rc = rc or (s if s > 0 else 128 - s)
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
+def dist_setup(gpus: int):
+    """World size from the launcher's env (torchrun); it must agree with
+    --gpus.  Fails loudly instead of silently measuring fewer GPUs."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}; "
+                         "launch with --gpus equal to the rank count")
     if os.environ.get("YRSS_BENCH_ONE_DEVICE"):
         local = 0            # rehearsal of the N>1 path on a single GPU
     if world > 1:
@@ -92,6 +142,32 @@ def dist_setup():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     return world, rank, local
+
+
+def device_identity(local: int, dry: bool) -> str:
+    """PCI location (domain:bus:device) of the GPU this rank drives."""
+    if dry:    # the test hook stands in for two ranks opening one device
+        return "dry-device" if os.environ.get("YRSS_BENCH_FAKE_SAME_DEVICE") \
+            else f"dry-rank-local{local}"
+    import torch
+
+    p = torch.cuda.get_device_properties(local)
+    dom = getattr(p, "pci_domain_id", 0)
+    bus = getattr(p, "pci_bus_id", None)
+    dev = getattr(p, "pci_device_id", None)
+    if bus is None:
+        return f"{p.name}#{local}"
+    return f"{dom:04x}:{bus:02x}:{dev:02x}"
+
+
+def gather_objects(obj, world: int):
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def barrier(world):
@@ -269,9 +345,49 @@ def load_traffic(path: str, key: dict):
     return None
 
 
+def check_devices(ident: str, world: int):
+    """Every rank's device; N ranks must drive N distinct GPUs (except the
+    declared one-device rehearsal, YRSS_BENCH_ONE_DEVICE)."""
+    devs = gather_objects(ident, world)
+    if len(set(devs)) != len(devs) and not os.environ.get("YRSS_BENCH_ONE_DEVICE"):
+        raise SystemExit(f"bench.py: ranks share a device: {devs}")
+    return devs
+
+
+def dry_run(args, world, rank, local):
+    """The timed loop's plumbing with the GPU work left out (--dry): spawn,
+    barriers, max-over-ranks time, sum of packets, device check.  For CPU
+    tests of the N>1 launch; the line says dry and carries no value."""
+    devices = check_devices(device_identity(local, True), world)
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    t1 = time.perf_counter()
+    barrier(world)
+    elapsed = max_over_ranks(t1 - t0, world)
+    total = sum_over_ranks(float(args.pkts * args.steps), world)
+    if rank == 0:
+        print(json.dumps({"metric": "dry run (no GPU work)", "dry": True, "value": None,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "pkts_total": total, "elapsed_s": elapsed,
+                          "config": {"parallelism": f"shard{world}", "devices": devices}}),
+              flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+    return 0
+
+
 def main(argv=None):
-    args = parse_args(argv)
-    world, rank, local = dist_setup()
+    raw = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(raw)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus, raw)
+    world, rank, local = dist_setup(args.gpus)
+    if args.dry:
+        return dry_run(args, world, rank, local)
     import numpy as np
     import torch
 
@@ -279,6 +395,7 @@ def main(argv=None):
     from yastack_amd.shard import shard_range
 
     torch.cuda.set_device(local)
+    devices = check_devices(device_identity(local, False), world)
     nbq = args.nb_queues or args.nb_procs
     eng = SoftRss(nb_procs=args.nb_procs, nb_queues=nbq, soft_dispatch=1,
                   dispatch_only_core=args.dispatch_only_core, device=local, max_burst=0)
@@ -385,6 +502,7 @@ def main(argv=None):
                 "per_queue_lists": not args.no_compact,
                 "kni_filter": args.filter,
                 "parallelism": f"shard{world}",
+                "devices": devices,
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -411,4 +529,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

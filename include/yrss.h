@@ -278,7 +278,11 @@ int yrss_dispatch_frames(yrss_ctx *ctx, const uint8_t *const *data,
  * context, so yrss_set_dispatch_ctx names the one to use (NULL clears it;
  * yrss_fini clears it for its own context).  Every call is a one-packet GPU
  * burst with its own launch and synchronisation (~15 µs): a drop-in for
- * registration, not the fast path — use the burst hook or the worker. */
+ * registration, not the fast path — use the burst hook or the worker.
+ * Calls from several threads (soft_dispatch=0 runs the dispatcher on every
+ * lcore, ff_dpdk_if.c:1653) are serialised by one process-wide mutex.  Give the
+ * shim a context of its own: while that context has a YRSS_F_ASYNC burst
+ * pending the call returns -1, and F-Stack frees the mbuf. */
 int yrss_set_dispatch_ctx(yrss_ctx *ctx);
 int yrss_toeplitz_dispatch(void *data, uint16_t len, uint16_t queue_id, uint16_t nb_queues);
 

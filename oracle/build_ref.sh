@@ -11,7 +11,8 @@
 # needs DPDK headers that require DPDK's generated rte_build_config.h, which
 # the image lacks, so it is unbuildable here.
 #
-# Output: oracle/_ref/libref_thash.so (git-ignored, travels to the GPU box).
+# Output: oracle/_ref/libref_thash.so (git-ignored, and listed in .gpurunignore:
+# no reference-compiled object goes to the GPU box).
 set -eu
 HERE=$(cd "$(dirname "$0")" && pwd)
 REF=${YRSS_REFERENCE:-/root/reference}

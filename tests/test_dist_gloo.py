@@ -38,7 +38,7 @@ def _worker(rank, world, port, q):
     from oracle import oracle
     from yastack_amd.shard import merge_queue_lists, shard_range
 
-    w, r, _ = bench.dist_setup()
+    w, r, _ = bench.dist_setup(world)
     assert (w, r) == (world, rank)
     first, cnt = shard_range(N_TOTAL, world, rank)
     win, lens = oracle.synth(6, cnt, first, stride=80)

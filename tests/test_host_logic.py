@@ -129,3 +129,8 @@ def test_dispatch_dev_refuses_short_buffers():
     with pytest.raises(ValueError):
         _check_dev_sizes(100, 64, T(6400, 1), T(100, 2),
                          DispatchResult(T(100, 2), T(100, 4), T(100, 4), T(3, 4)), 3)
+    # the kernels write nb_queues+2 offsets (qstart[nb_queues+1] == n): a
+    # nb_queues+1 array would take a 4-byte store past its end
+    with pytest.raises(ValueError):
+        _check_dev_sizes(100, 64, T(6400, 1), T(100, 2),
+                         DispatchResult(T(100, 2), T(100, 4), T(100, 4), T(4, 4)), 3)

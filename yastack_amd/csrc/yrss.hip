@@ -2224,8 +2224,13 @@ uint64_t mono_ns()
 }
 
 // Context behind yrss_toeplitz_dispatch: dispatch_func_t has no context
-// argument (ff_api.h:167), so the registration shim reads this one.
+// argument (ff_api.h:167), so the registration shim reads this one.  The
+// mutex serialises shim calls: with soft_dispatch=0 every lcore calls the
+// registered dispatcher (ff_dpdk_if.c:1653,1078), and one context's staging
+// and burst state take one burst at a time.  yrss_fini takes it too, so a
+// context is never torn down under a running shim call.
 yrss_ctx *g_dispatch_ctx = nullptr;
+std::mutex g_dispatch_mu;
 
 // A scan look-back that never resolved leaves that batch's lists invalid.
 bool take_scan_fault(yrss_ctx *c)
@@ -2621,9 +2626,11 @@ void yrss_fini(yrss_ctx *c)
     if (!c)
         return;
     (void)hipSetDevice(c->device);
-    yrss_ctx *self = c;
-    __atomic_compare_exchange_n(&g_dispatch_ctx, &self, (yrss_ctx *)nullptr, false,
-                                __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
+    {
+        std::lock_guard<std::mutex> lk(g_dispatch_mu);
+        if (g_dispatch_ctx == c)
+            g_dispatch_ctx = nullptr;
+    }
     if (c->w.on) {
         (void)worker_halt(c);
         worker_free(c);
@@ -2908,7 +2915,8 @@ int yrss_dispatch_frames(yrss_ctx *c, const uint8_t *const *data, const uint16_t
 
 int yrss_set_dispatch_ctx(yrss_ctx *c)
 {
-    __atomic_store_n(&g_dispatch_ctx, c, __ATOMIC_RELEASE);
+    std::lock_guard<std::mutex> lk(g_dispatch_mu);
+    g_dispatch_ctx = c;
     return 0;
 }
 
@@ -2921,7 +2929,8 @@ int yrss_toeplitz_dispatch(void *data, uint16_t len, uint16_t queue_id, uint16_t
 {
     (void)queue_id;
     (void)nb_queues;
-    yrss_ctx *c = __atomic_load_n(&g_dispatch_ctx, __ATOMIC_ACQUIRE);
+    std::lock_guard<std::mutex> lk(g_dispatch_mu);
+    yrss_ctx *c = g_dispatch_ctx;
     if (!c || !data) {
         // the contract's only error channel (ff_api.h:148-166): F-Stack frees the mbuf
         static bool warned = false;

@@ -65,7 +65,7 @@ def _check_dev_sizes(n, stride, win, lens, out, nb_queues):
     if out.qidx is not None:
         need.append(("qidx", out.qidx, 4 * n))
     if out.qstart is not None:
-        need.append(("qstart", out.qstart, 4 * (nb_queues + 1)))
+        need.append(("qstart", out.qstart, 4 * (nb_queues + 2)))
     if out.filter is not None:
         need.append(("filter", out.filter, n))
     for name, t, b in need:
