@@ -7,6 +7,6 @@ IFS=';' read -r -a VARS <<< "${AB_VARIANTS:-YRSS_AHEAD=1;YRSS_AHEAD=2}"
 for r in $(seq 1 "${AB_ROUNDS:-3}"); do
   for v in "${VARS[@]}"; do
     env $v timeout -k 10 300 python bench.py --cpu-seconds 0 --pcie 0 ${BENCH_ARGS:-} > gpurun_out/ab.log 2>&1 || { tail gpurun_out/ab.log; exit 1; }
-    echo "[$v] $(tail -1 gpurun_out/ab.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], d["ms_per_step"], r["kernel_avg_us"], r["probe"] and r["probe"]["us"], d["check"]["bit_exact"])')"
+    echo "[$v] $(tail -1 gpurun_out/ab.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); r=d["roofline"]; print(d["value"], d["ms_per_step"], r["kernel_avg_us"], r["probe"] and r["probe"]["us"], d["check"] and d["check"]["bit_exact"])')"
   done
 done

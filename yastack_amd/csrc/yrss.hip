@@ -57,7 +57,25 @@ constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
 constexpr int kScatterRound = 8;       // packets per lane per scatter round
 constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this many buckets
 constexpr uint32_t kRankStage = 1024;   // ranked scatter: chunk stage (packets) per wave
-constexpr int kTblBytes = 12 * 256 * 4;
+constexpr uint32_t kImgPkts = 4096;     // few-bucket scatter: largest group built in LDS
+constexpr uint32_t kImgLine = 32;       // entries per 128-byte line
+constexpr uint32_t kImgWords = kImgPkts + 8u * 2u * kImgLine;   // + up to 2 lines of slack per bucket
+// Toeplitz key tables: the 96 tuple bits are cut into fields of kHashBits
+// (MSB first); table t maps a field value to the XOR of the key windows its
+// set bits select.  8: 12 byte tables of 256 words (12 lookups; random indices
+// over 8 rows of the 32 banks a ds_read_b32 half-wave uses, ~4-way
+// conflicts).  4: 24 nibble tables of 16 words (24 lookups; a table spans 16
+// distinct banks, so a half-wave's reads never conflict).
+#ifndef YRSS_HASH_BITS
+#define YRSS_HASH_BITS 8
+#endif
+constexpr int kHashBits = YRSS_HASH_BITS;
+static_assert(kHashBits == 4 || kHashBits == 8, "field width divides 32");
+constexpr int kFieldsPerWord = 32 / kHashBits;
+constexpr int kTblEntries = 1 << kHashBits;
+constexpr int kTblWordsPerTupleWord = kFieldsPerWord * kTblEntries;
+constexpr int kTblWords = 3 * kTblWordsPerTupleWord;
+constexpr int kTblBytes = kTblWords * 4;
 constexpr int kRsrcWord3 = 0x00020000;  // buffer resource dword 3 for gfx9-family (CDNA)
 constexpr uint32_t kOutTiles = 4;       // parse: output burst (tiles buffered in LDS)
 constexpr int kOutBytes = kOutTiles * kTile * (4 + 2 + 1 + 2);   // hash, q, filter, rank
@@ -107,6 +125,7 @@ struct ScatterParams {
     uint32_t gshift;           // a group is 2^gshift chunks
     uint32_t chunk;            // packets per chunk
     const uint16_t *rank;      // ranked mode: rank in chunk per packet (parse kCount == 2)
+    uint32_t img;              // few-bucket groups assemble their lists in LDS (seg <= kImgPkts)
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -187,10 +206,47 @@ __device__ __forceinline__ uint32_t win_byte(const ParseParams &P, const uint32_
 // Toeplitz over one 32-bit tuple word (bit 31-k selects key window k), the two
 // ways: four lookups into byte tables tb[j*256+v] (v = byte j of the word from
 // the top), or bit-serial on the VALU with the windows in SGPRs.
+__device__ __forceinline__ uint32_t field_of(uint32_t w, int f)
+{
+    const int pos = 32 - (f + 1) * kHashBits;
+    if constexpr (kHashBits == 8)
+        return (w >> pos) & 0xffu;
+    // v_bfe_u32 by hand: left to itself the compiler turns (w >> pos) & 15
+    // into a pre-scaled (w >> (pos-2)) & 60 and then cannot fold the LDS base
+    // into v_lshl_add_u32, one VALU op more per lookup
+    uint32_t x;
+    asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(x) : "v"(w), "i"(pos), "i"(kHashBits));
+    return x;
+}
+
 __device__ __forceinline__ uint32_t tz_lds(uint32_t w, const uint32_t *tb)
 {
-    return tb[w >> 24] ^ tb[256 + ((w >> 16) & 0xffu)] ^ tb[512 + ((w >> 8) & 0xffu)] ^
-           tb[768 + (w & 0xffu)];
+    uint32_t v[kFieldsPerWord];
+#pragma unroll
+    for (int f = 0; f < kFieldsPerWord; ++f)
+        v[f] = tb[f * kTblEntries + field_of(w, f)];
+    if constexpr (kFieldsPerWord == 4) {
+        return v[0] ^ v[1] ^ v[2] ^ v[3];
+    } else {   // 8 nibble lookups: xor3 tree (v_bitop3 0x96)
+        const uint32_t a = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96);
+        const uint32_t b = __builtin_amdgcn_bitop3_b32(v[3], v[4], v[5], 0x96);
+        return __builtin_amdgcn_bitop3_b32(a, b, v[6] ^ v[7], 0x96);
+    }
+}
+
+// Table t, value v: XOR of key windows kwin[t*kHashBits + b] over v's set
+// bits b (b = 0 is v's most significant bit).  Threads tid, tid+nthr, ...
+__device__ __forceinline__ void build_key_tables(uint32_t *tbl, const uint32_t *kwin,
+                                                 uint32_t tid, uint32_t nthr)
+{
+    for (uint32_t e = tid; e < (uint32_t)kTblWords; e += nthr) {
+        const uint32_t t = e >> kHashBits, v = e & (kTblEntries - 1u);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int b = 0; b < kHashBits; ++b)
+            acc ^= (v & (1u << (kHashBits - 1 - b))) ? kwin[kHashBits * t + b] : 0u;
+        tbl[e] = acc;
+    }
 }
 
 __device__ __forceinline__ uint32_t tz_valu(uint32_t w, const uint32_t *kw, uint32_t h)
@@ -392,6 +448,11 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
         const uint32_t w0 = __builtin_amdgcn_alignbit(d7, d6, 16);
         const uint32_t w1 = __builtin_amdgcn_alignbit(d8, d7, 16);
         uint32_t h_l3 = 0;
+        const uint32_t w2 = (pa & 0xffff0000u) | (pb & 0xffffu);
+#if defined(YRSS_DIAG) && (YRSS_DIAG & 1)
+        // diagnosis build only (wrong hashes): no table lookups
+        h = h_l3 = w0 ^ w1 ^ w2;
+#else
         if (kVw > 0)
             h_l3 = tz_valu(w0, P.kwin, h_l3);
         else
@@ -399,12 +460,12 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
         if (kVw > 1)
             h_l3 = tz_valu(w1, P.kwin + 32, h_l3);
         else
-            h_l3 ^= tz_lds(w1, tbl + 4 * 256);
-        const uint32_t w2 = (pa & 0xffff0000u) | (pb & 0xffffu);
+            h_l3 ^= tz_lds(w1, tbl + kTblWordsPerTupleWord);
         if (kVw > 2)
             h = tz_valu(w2, P.kwin + 64, h_l3);
         else
-            h = h_l3 ^ tz_lds(w2, tbl + 8 * 256);
+            h = h_l3 ^ tz_lds(w2, tbl + 2 * kTblWordsPerTupleWord);
+#endif
         bool trunc = false;
         // Rare slow path, entered only by waves that hold such a packet, so its
         // global loads (and the vmcnt drain they imply) stay off the hot loop.
@@ -414,21 +475,39 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
                     reinterpret_cast<const uint32_t *>(P.win + (size_t)pkt * P.stride);
                 const uint32_t ta = __builtin_nontemporal_load(g + j);
                 const uint32_t tb = __builtin_nontemporal_load(g + j + 1u);
-                h = h_l3 ^ tz_lds((ta & 0xffff0000u) | (tb & 0xffffu), tbl + 8 * 256);
+                h = h_l3 ^ tz_lds((ta & 0xffff0000u) | (tb & 0xffffu), tbl + 2 * kTblWordsPerTupleWord);
             } else {
                 trunc = true;
             }
         }
         // hash % d exactly (Lemire fastmod, 64-bit M), then +q_off (:2031-2034)
+#if defined(YRSS_DIAG) && (YRSS_DIAG & 2)
+        const uint32_t rem = h & 1u;   // diagnosis build only: no fastmod
+#else
         const uint64_t low = P.mod_m * (uint64_t)h;
         const uint32_t rem = (uint32_t)__umul64hi(low, (uint64_t)P.mod_d);
+#endif
         qv = (int)(uint16_t)(rem + P.q_off);
         if (trunc) {
             qv = YRSS_Q_TRUNCATED;
             h = 0u;
         }
+#if defined(YRSS_DIAG) && (YRSS_DIAG & 4)
+        qv = YRSS_DEFAULT_Q;   // diagnosis build only: one bucket, as UDP
+#endif
+#if defined(YRSS_DIAG) && (YRSS_DIAG & 32)
+        // diagnosis build only: one bucket, the block kept alive (P.n != 0)
+        qv = YRSS_DEFAULT_Q + (int)(rem * (P.n == 0u));
+#endif
+#if defined(YRSS_DIAG) && (YRSS_DIAG & 12)
+        h = 0u;                // diagnosis build only: zero hash words, as UDP
+#endif
     }
 
+#if defined(YRSS_DIAG) && (YRSS_DIAG & 16)
+    if (!hashed)   // diagnosis build only: two buckets without the hash block
+        qv = 1 + (int)(pkt & 1u);
+#endif
     int fc = kFilterUnknown;
     if (kFilter) {
         // protocol_filter (ff_dpdk_if.c:976-996) + ff_kni_proto_filter
@@ -521,15 +600,7 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     const uint32_t gw = blockIdx.x * kWaves + wave;
     const uint32_t W = gridDim.x * kWaves;
 
-    // Byte tables: tbl[j*256+v] = XOR of key windows at bits 8j+b, v's bit b set.
-    for (uint32_t e = threadIdx.x; e < 12u * 256u; e += kBlock) {
-        const uint32_t jt = e >> 8, v = e & 255u;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-            acc ^= (v & (0x80u >> b)) ? P.kwin[8 * jt + b] : 0u;
-        tbl[e] = acc;
-    }
+    build_key_tables(tbl, P.kwin, threadIdx.x, kBlock);
     if (kFilter)
         for (uint32_t e = threadIdx.x; e < (uint32_t)kKniWords; e += kBlock)
             kni[e] = P.kni_enable ? P.kni_bm[e] : 0u;
@@ -731,7 +802,7 @@ __device__ __forceinline__ void load_round(const int16_t *q, uint32_t r0, uint32
 // needs no LDS, and stores go straight from registers.  q of the next round is
 // in flight while a round is ranked.
 __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const uint32_t *gcnt,
-                            uint32_t beg, uint32_t end, uint32_t lane)
+                            uint32_t beg, uint32_t end, uint32_t lane, uint32_t *img)
 {
     uint32_t ub[kFewBuckets], cur[kFewBuckets];
 #pragma unroll
@@ -774,6 +845,25 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const u
             P.qidx[d + t] = beg + t;
         return;
     }
+    // LDS image (img != null): bucket k's list run [cur0, cur0 + cnt) is
+    // assembled at img[cur + ioff[k]], ioff aligning the run's 128-byte lines
+    // to the image, then leaves as whole lines of 16-byte non-temporal stores.
+    // Plain per-lane stores left the lists' lines dirty in the caches, and
+    // their write-back then ran inside the NEXT batch's parse kernel (+15-17 us
+    // on all-TCP at 2^24 packets, while that kernel's own traffic was at the
+    // probe floor; non-temporal per-lane stores wrote partial lines, 1.6x).
+    uint32_t ioff[kFewBuckets], c0[kFewBuckets];
+    if (img) {
+        uint32_t base = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kFewBuckets; ++k) {
+            c0[k] = cur[k];
+            const uint32_t cnt = k < K ? gcnt[ub[k]] : 0u;
+            ioff[k] = base - (cur[k] & ~(kImgLine - 1u));
+            base += k < K ? (((cur[k] & (kImgLine - 1u)) + cnt + kImgLine - 1u) & ~(kImgLine - 1u))
+                          : 0u;
+        }
+    }
     constexpr uint32_t kRound = kWave * kScatterRound;
     int32_t nxt[kScatterRound];
     load_round(P.q, beg, end, lane, nxt);
@@ -804,11 +894,18 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const u
                     const uint64_t M = __ballot(hit) & vb[j];
                     const uint32_t r = __builtin_amdgcn_mbcnt_hi(
                         (uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, base));
-                    dst[j] = hit ? r : dst[j];
+                    dst[j] = hit ? r + (img ? ioff[k] : 0u) : dst[j];
                     base += (uint32_t)__popcll(M);
                 }
                 cur[k] = base;
             }
+        }
+        if (img) {
+#pragma unroll
+            for (int j = 0; j < kScatterRound; ++j)
+                if ((vb[j] >> lane) & 1u)
+                    img[dst[j]] = r0 + j * kWave + lane;
+            continue;
         }
 #pragma unroll
         for (int j = 0; j < kScatterRound; ++j)
@@ -817,6 +914,36 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const u
                 // partial lines (non-temporal ones cost 1.6x here)
                 P.qidx[dst[j]] = r0 + j * kWave + lane;
             }
+    }
+    if (!img)
+        return;
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t k = 0; k < kFewBuckets; ++k) {
+        if (k >= K)
+            break;
+        const uint32_t a = c0[k], e = cur[k];   // this group's run of bucket ub[k]
+        const uint32_t la = (a + kImgLine - 1u) & ~(kImgLine - 1u);
+        const uint32_t le = e & ~(kImgLine - 1u);
+        const uint32_t io = ioff[k];   // image index of global slot g: g + io (mod 2^32)
+        if (la < le) {
+            // whole lines: 16-byte non-temporal stores, 1 KiB per wave-instruction
+            const uint32_t nv = (le - la) >> 2;
+            for (uint32_t v = lane; v < nv; v += kWave) {
+                const uint32_t g = la + 4u * v;
+                const u32x4 x = *reinterpret_cast<const u32x4 *>(img + (g + io));
+                __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(P.qidx + g));
+            }
+            // the partial lines at both ends are shared with the neighbouring
+            // groups' runs: plain 4-byte stores, merged in L2
+            if (lane < la - a)
+                P.qidx[a + lane] = img[a + lane + io];
+            if (lane < e - le)
+                P.qidx[le + lane] = img[le + lane + io];
+        } else {
+            for (uint32_t g = a + lane; g < e; g += kWave)
+                P.qidx[g] = img[g + io];
+        }
     }
 }
 
@@ -934,7 +1061,10 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
     const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
     if (kseg <= kFewBuckets)
-        scatter_few(P, off, gcnt, beg, end, lane);
+        scatter_few(P, off, gcnt, beg, end, lane,
+                    P.img ? reinterpret_cast<uint32_t *>(smem) + kScatterWaves * 2u * P.nb +
+                                wave * kImgWords
+                          : nullptr);
     else
         scatter_general(P, off, beg, end, lane);
 }
@@ -1377,14 +1507,7 @@ __device__ __forceinline__ SmallLds small_carve(uint8_t *smem, uint32_t wave, ui
 template <bool kFilter>
 __device__ __forceinline__ void small_tables(const ParseParams &P, const SmallLds &L)
 {
-    for (uint32_t e = threadIdx.x; e < 12u * 256u; e += kSmallBlock) {
-        const uint32_t jt = e >> 8, v = e & 255u;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int b = 0; b < 8; ++b)
-            acc ^= (v & (0x80u >> b)) ? P.kwin[8 * jt + b] : 0u;
-        L.tbl[e] = acc;
-    }
+    build_key_tables(L.tbl, P.kwin, threadIdx.x, kSmallBlock);
     if (kFilter)
         for (uint32_t e = threadIdx.x; e < (uint32_t)kKniWords; e += kSmallBlock)
             L.kni[e] = P.kni_enable ? P.kni_bm[e] : 0u;
@@ -1833,6 +1956,7 @@ struct yrss_ctx {
     uint32_t group_tiles = 0;       // 0: 64
     uint16_t *d_rank = nullptr;     // ranked mode workspace (n x u16), grown on demand
     bool no_rank = false;           // YRSS_NO_RANK: ballot scatter even for many buckets
+    bool no_img = false;            // YRSS_NO_IMG: few-bucket lists stored per lane, not via LDS
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
     uint32_t *d_scan_fault = nullptr;   // host-coherent pinned word (yrss_status)
@@ -2542,6 +2666,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     }
     if (const char *e = getenv("YRSS_NO_RANK"))
         c->no_rank = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_NO_IMG"))
+        c->no_img = atoi(e) != 0;
     if (const char *e = getenv("YRSS_GROUP_TILES")) {
         const int v = atoi(e);
         if (v >= 1 && v <= 65536)
@@ -2840,6 +2966,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.gshift = lay.shift;
     S.chunk = lay.chunk;
     S.rank = c->d_rank;
+    // few-bucket groups build their lists in LDS when a group fits the image
+    S.img = (!ranked && lay.seg <= kImgPkts && !c->no_img) ? 1u : 0u;
     {
         Timed t(c, YRSS_K_SCATTER);
         if (ranked)
@@ -2851,8 +2979,9 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         else
             hipExtLaunchKernelGGL(yrss_scatter, dim3(lay.nseg / kScatterWaves),
                                   dim3(kScatterBlock),
-                                  (uint32_t)(kScatterWaves * 2u * c->nb * sizeof(uint32_t)), s,
-                                  t.a, t.b, 0, S);
+                                  (uint32_t)(kScatterWaves * (2u * c->nb + (S.img ? kImgWords : 0u)) *
+                                             sizeof(uint32_t)),
+                                  s, t.a, t.b, 0, S);
     }
     YRSS_HIP(hipGetLastError());
     return 0;
