@@ -2,7 +2,9 @@
 # outputs wrong, so --check 0): 1 no table lookups, 2 no fastmod, 8 hash words
 # written as 0, 4 one bucket (q = 2; the compiler then drops the whole hashed
 # block), 32 one bucket with the hashed block kept, 16 UDP packets spread over
-# two buckets (no hashed block).  Build: for v in ...; do mkdir -p build/dg$v;
+# two buckets (no hashed block); 128 few-bucket scatter with non-temporal
+# per-lane stores.  The switches live in commit 4d8d485 (removed after).
+# Build from that commit: for v in ...; do mkdir -p build/dg$v;
 # hipcc <build() flags> -DYRSS_DIAG=$v ... -o build/dg$v/libyrss.so; done
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp PYTHONUNBUFFERED=1

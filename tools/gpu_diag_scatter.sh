@@ -1,6 +1,6 @@
 # Does the few-bucket scatter's plain-store output (64 MB of qidx left dirty in
 # the caches) get written back during the NEXT parse kernel?  dg128 = the same
-# build with non-temporal scatter stores.  Parse µs (kernel_avg_us) and step
+# build with non-temporal scatter stores (YRSS_DIAG, commit 4d8d485).  Parse µs (kernel_avg_us) and step
 # time per variant, plus rocprof per-kernel stats of each.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp PYTHONUNBUFFERED=1

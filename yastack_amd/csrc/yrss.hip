@@ -449,10 +449,6 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
         const uint32_t w1 = __builtin_amdgcn_alignbit(d8, d7, 16);
         uint32_t h_l3 = 0;
         const uint32_t w2 = (pa & 0xffff0000u) | (pb & 0xffffu);
-#if defined(YRSS_DIAG) && (YRSS_DIAG & 1)
-        // diagnosis build only (wrong hashes): no table lookups
-        h = h_l3 = w0 ^ w1 ^ w2;
-#else
         if (kVw > 0)
             h_l3 = tz_valu(w0, P.kwin, h_l3);
         else
@@ -465,7 +461,6 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
             h = tz_valu(w2, P.kwin + 64, h_l3);
         else
             h = h_l3 ^ tz_lds(w2, tbl + 2 * kTblWordsPerTupleWord);
-#endif
         bool trunc = false;
         // Rare slow path, entered only by waves that hold such a packet, so its
         // global loads (and the vmcnt drain they imply) stay off the hot loop.
@@ -481,33 +476,15 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
             }
         }
         // hash % d exactly (Lemire fastmod, 64-bit M), then +q_off (:2031-2034)
-#if defined(YRSS_DIAG) && (YRSS_DIAG & 2)
-        const uint32_t rem = h & 1u;   // diagnosis build only: no fastmod
-#else
         const uint64_t low = P.mod_m * (uint64_t)h;
         const uint32_t rem = (uint32_t)__umul64hi(low, (uint64_t)P.mod_d);
-#endif
         qv = (int)(uint16_t)(rem + P.q_off);
         if (trunc) {
             qv = YRSS_Q_TRUNCATED;
             h = 0u;
         }
-#if defined(YRSS_DIAG) && (YRSS_DIAG & 4)
-        qv = YRSS_DEFAULT_Q;   // diagnosis build only: one bucket, as UDP
-#endif
-#if defined(YRSS_DIAG) && (YRSS_DIAG & 32)
-        // diagnosis build only: one bucket, the block kept alive (P.n != 0)
-        qv = YRSS_DEFAULT_Q + (int)(rem * (P.n == 0u));
-#endif
-#if defined(YRSS_DIAG) && (YRSS_DIAG & 12)
-        h = 0u;                // diagnosis build only: zero hash words, as UDP
-#endif
     }
 
-#if defined(YRSS_DIAG) && (YRSS_DIAG & 16)
-    if (!hashed)   // diagnosis build only: two buckets without the hash block
-        qv = 1 + (int)(pkt & 1u);
-#endif
     int fc = kFilterUnknown;
     if (kFilter) {
         // protocol_filter (ff_dpdk_if.c:976-996) + ff_kni_proto_filter
