@@ -1,8 +1,8 @@
 #!/bin/sh
 # ORACLE — TEST INFRASTRUCTURE ONLY.
 #
-# Compile the reference's own Toeplitz engine from its source, where it lies,
-# into oracle/_ref/libref_thash.so.  Two pieces of fs/lib/ff_dpdk_if.c need
+# Compile the reference's own Toeplitz engine and KNI port-bitmap parser from
+# their source, where they lie, into oracle/_ref/libref_{thash,kni}.so.  Two pieces of fs/lib/ff_dpdk_if.c need
 # nothing beyond the C library and are compiled verbatim:
 #   default_rsskey_40bytes   ff_dpdk_if.c:113-119
 #   toeplitz_hash            ff_dpdk_if.c:1881-1902
@@ -48,3 +48,31 @@ EOF
 } | ${CC:-gcc} -O2 -frename-registers -funswitch-loops -fweb -fPIC -shared -x c - \
       -o "$HERE/_ref/libref_thash.so"
 echo "build_ref.sh: built $HERE/_ref/libref_thash.so"
+
+# The KNI port bitmaps, fs/lib/ff_dpdk_kni.c: the bit macros and magic_bits
+# (:51-58), set_bitmap / get_bitmap (:83-96) and kni_set_bitmap (:98-123) need
+# only htons, strstr and atoi, so they too are compiled verbatim, streamed
+# from the reference file into gcc, into oracle/_ref/libref_kni.so.
+KNI="$REF/fs/lib/ff_dpdk_kni.c"
+if [ ! -f "$KNI" ]; then
+    echo "build_ref.sh: $KNI not present; libref_kni.so not built" >&2
+    exit 0
+fi
+{
+    printf '#include <stdint.h>\n#include <stdlib.h>\n#include <string.h>\n#include <arpa/inet.h>\n'
+    printf '#line 1 "%s"\n' "$KNI"
+    awk '/^#define (set|clear|get)_bit\(/ {print}' "$KNI"
+    awk '/^static const int magic_bits/ {f = 1} f {print} f && /^};/ {exit}' "$KNI"
+    for fn in set_bitmap get_bitmap kni_set_bitmap; do
+        awk -v fn="$fn" 'prev ~ /^static (void|int)[ \t]*$/ && index($0, fn "(") == 1 {print prev; f = 1}
+             f {print}
+             f && /^}/ {exit}
+             {prev = $0}' "$KNI"
+    done
+    cat <<'EOF2'
+void ref_kni_set_bitmap(const char *p, unsigned char *bm) { kni_set_bitmap(p, bm); }
+int ref_get_bitmap(uint16_t port, unsigned char *bm) { return get_bitmap(port, bm); }
+void ref_set_bitmap(uint16_t port, unsigned char *bm) { set_bitmap(port, bm); }
+EOF2
+} | ${CC:-gcc} -O2 -fPIC -shared -x c - -o "$HERE/_ref/libref_kni.so"
+echo "build_ref.sh: built $HERE/_ref/libref_kni.so"

@@ -16,6 +16,7 @@ import numpy as np
 HERE = Path(__file__).resolve().parent
 LIB = HERE / "liboracle.so"
 REF_LIB = HERE / "_ref" / "libref_thash.so"
+REF_KNI_LIB = HERE / "_ref" / "libref_kni.so"
 
 MLX_KEY = bytes.fromhex(
     "d181c62cf7f4db5b1983a2fc943e1adbd9389e6bd1039c2ca74499ad593d56d9f3253c062adc1ffc")
@@ -39,6 +40,7 @@ class SynthParams(ctypes.Structure):
 
 _lib = None
 _ref = None
+_ref_kni = None
 
 
 def build() -> None:
@@ -85,6 +87,27 @@ def lib() -> ctypes.CDLL:
                                             ctypes.c_int]
         _lib = L
     return _lib
+
+
+def ref_kni():
+    """The reference's compiled kni_set_bitmap / get_bitmap (oracle/_ref,
+    fs/lib/ff_dpdk_kni.c:51-123), or None if oracle/_ref is absent."""
+    global _ref_kni
+    if _ref_kni is None and REF_KNI_LIB.exists():
+        R = ctypes.CDLL(str(REF_KNI_LIB))
+        R.ref_kni_set_bitmap.restype = None
+        R.ref_kni_set_bitmap.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+        R.ref_get_bitmap.restype = ctypes.c_int
+        R.ref_get_bitmap.argtypes = [ctypes.c_uint16, ctypes.c_void_p]
+        _ref_kni = R
+    return _ref_kni
+
+
+def ref_kni_bitmap(ports: str | None) -> np.ndarray:
+    """The 8 KiB bitmap the reference's kni_set_bitmap builds from a port list."""
+    bm = np.zeros(8192, np.uint8)
+    ref_kni().ref_kni_set_bitmap(None if ports is None else ports.encode(), bm.ctypes.data)
+    return bm
 
 
 def ref():

@@ -75,12 +75,26 @@ def survey_kat():
     ]
     for name, f, L, q8 in edges:
         cases.append({"name": name, "frame": f.hex(), "len": L, "expect": {"np8": q8}})
+    # IHL=15, len 80 -> hashed, hash 0xc65b1882.  The survey did
+    # not record bytes 74..77 (the L4 ports at 14 + 4*15).  The hash is GF(2)-
+    # linear in the tuple bits, so with the edge cases' addresses (10.0.0.1 ->
+    # 10.0.0.2) the port bits follow from one linear solve (rank 31 of 32); its
+    # natural solution, sport 1 -> dport 2 (bytes 00 01 00 02), reproduces the
+    # recorded hash through the reference's own toeplitz_hash (asserted below).
+    f15 = ipv4_frame("10.0.0.1", 1, "10.0.0.2", 2, ihl=15, length=80)
+    R = oracle.ref()
+    if R is not None:
+        t = tuple_of(np.frombuffer(f15, np.uint8))
+        assert R.ref_toeplitz_hash(40, oracle.MLX_KEY, 12, t) == 0xC65B1882
+    cases.append({"name": "ihl15_len80", "frame": f15.hex(), "len": 80,
+                  "expect": {"hash": 0xC65B1882, "np8": 0xC65B1882 % 8}})
     return {
         "source": "SURVEY.md §8(a) known answers: reference toeplitz_dispatch "
                   "(fs/lib/ff_dpdk_if.c:1945-2113) run in the survey container, key "
                   "default_rsskey_40bytes (:113-119). Frames rebuilt by tests/frames.py.",
-        "not_asserted": "IHL=15 len=80 hash 0xc65b1882: the survey did not record the "
-                        "frame's bytes 74..77, so that row cannot be rebuilt.",
+        "reconstructed": "IHL=15 len=80 hash 0xc65b1882: bytes 74..77 (not recorded by the "
+                         "survey) solved from the hash's GF(2)-linearity; ports 1 -> 2 "
+                         "reproduce it through the reference toeplitz_hash.",
         "configs": {"np8": [8, 8, 1, 0], "np3": [3, 3, 0, 0], "np3_doc": [3, 3, 1, 1]},
         "cases": cases,
     }

@@ -103,3 +103,78 @@ def test_route_model_semantics(oracle_mod):
     assert ("clone", 2, 1) in freed and ("pkt", 5) in freed and ("pkt", 3) in freed
     assert local == [("pkt", 2)]                    # ARP stays local too
     assert kni == [("clone", 2, 0xFFFF), ("pkt", 4)]  # KNI clone of ARP, KNI-accepted pkt
+
+
+# ---- pinned to the reference itself: oracle/_ref/libref_kni.so is
+# fs/lib/ff_dpdk_kni.c:51-123 compiled verbatim by oracle/build_ref.sh ----------
+
+def _ref_or_skip(oracle_mod):
+    import pytest
+
+    if oracle_mod.ref_kni() is None:
+        pytest.skip("oracle/_ref/libref_kni.so not built (reference not mounted)")
+
+
+def _random_port_list(rng):
+    def num():
+        r = rng.random()
+        if r < 0.05:
+            return str(int(rng.integers(-5, 1)))
+        if r < 0.1:
+            return str(int(rng.integers(65530, 70001)))
+        return str(int(rng.integers(0, 65536)))
+
+    pieces = []
+    for _ in range(int(rng.integers(1, 6))):
+        k = rng.random()
+        if k < 0.4:
+            pieces.append(num())
+        elif k < 0.7:
+            lo = int(rng.integers(0, 65536))
+            pieces.append(f"{lo}-{min(lo + int(rng.integers(-3, 300)), 70000)}")
+        elif k < 0.76:
+            pieces.append(num() + "-")           # '-' right before ',' (tail_num < tail - 1)
+        elif k < 0.82:
+            pieces.append("-" + num())
+        elif k < 0.86:
+            pieces.append("")                   # empty field
+        elif k < 0.9:
+            pieces.append(" " + num())          # atoi skips leading blanks
+        elif k < 0.94:
+            pieces.append(f"{num()}-{num()}-{num()}")
+        else:
+            pieces.append(rng.choice(["abc", "0x50", "80a", "-", "--", "8-0-"]))
+    return ",".join(pieces)
+
+
+def test_kni_set_bitmap_vs_reference(oracle_mod):
+    _ref_or_skip(oracle_mod)
+    fixed = ["80", "80,443", "8000-8080", "80-", "-5", "90-80", "0-70000", "", ",", "80,,443",
+             "65535", "65536", "65537", "-1", "1-", "a-b", "1,2-", "5-,7", "0", "10-20,15-25"]
+    for s in fixed + [None]:
+        assert np.array_equal(oracle_mod.kni_bitmap(s), oracle_mod.ref_kni_bitmap(s)), s
+    rng = np.random.default_rng(20261016)
+    for _ in range(3000):
+        s = _random_port_list(rng)
+        assert np.array_equal(oracle_mod.kni_bitmap(s), oracle_mod.ref_kni_bitmap(s)), s
+
+
+def test_port_lookup_vs_reference_get_bitmap(oracle_mod):
+    """protocol_filter's port test (ff_dpdk_kni.c:232-236, 244-248) against the
+    reference's get_bitmap on the dst_port as stored (network order read as a
+    little-endian uint16)."""
+    _ref_or_skip(oracle_mod)
+    R = oracle_mod.ref_kni()
+    rng = np.random.default_rng(7)
+    for trial in range(6):
+        spec = _random_port_list(rng)
+        tcp = oracle_mod.kni_bitmap(spec)
+        udp = oracle_mod.kni_bitmap(_random_port_list(rng))
+        ports = list(rng.integers(0, 65536, 300)) + [80, 443, 0, 65535]
+        for dport in ports:
+            dport = int(dport)
+            raw = ((dport & 0xFF) << 8) | (dport >> 8)     # LE read of the network bytes
+            for proto, bm in ((6, tcp), (17, udp)):
+                f = ipv4_frame("10.0.0.1", 1234, "10.0.0.2", dport, proto=proto)
+                want = 2 if R.ref_get_bitmap(raw, bm.ctypes.data) else -1
+                assert oracle_mod.protocol_filter(f, 64, True, tcp, udp) == want, (spec, dport)
