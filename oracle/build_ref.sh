@@ -1,8 +1,9 @@
 #!/bin/sh
 # ORACLE — TEST INFRASTRUCTURE ONLY.
 #
-# Compile the reference's own Toeplitz engine and KNI port-bitmap parser from
-# their source, where they lie, into oracle/_ref/libref_{thash,kni}.so.  Two pieces of fs/lib/ff_dpdk_if.c need
+# Compile the reference's own Toeplitz engine, KNI port-bitmap parser and INI
+# reader from their source, where they lie, into oracle/_ref/libref_{thash,
+# kni,ini}.so.  Two pieces of fs/lib/ff_dpdk_if.c need
 # nothing beyond the C library and are compiled verbatim:
 #   default_rsskey_40bytes   ff_dpdk_if.c:113-119
 #   toeplitz_hash            ff_dpdk_if.c:1881-1902
@@ -48,6 +49,15 @@ EOF
 } | ${CC:-gcc} -O2 -frename-registers -funswitch-loops -fweb -fPIC -shared -x c - \
       -o "$HERE/_ref/libref_thash.so"
 echo "build_ref.sh: built $HERE/_ref/libref_thash.so"
+
+# The INI reader fs/lib vendors (inih, fs/lib/ff_ini_parser.c + .h) is plain
+# C: compiled where it lies into oracle/_ref/libref_ini.so, the checker of
+# yastack_amd/ffconfig.py's reader (tests/test_ffconfig.py).
+INI="$REF/fs/lib/ff_ini_parser.c"
+if [ -f "$INI" ]; then
+    ${CC:-gcc} -O2 -fPIC -shared "$INI" -o "$HERE/_ref/libref_ini.so"
+    echo "build_ref.sh: built $HERE/_ref/libref_ini.so"
+fi
 
 # The KNI port bitmaps, fs/lib/ff_dpdk_kni.c: the bit macros and magic_bits
 # (:51-58), set_bitmap / get_bitmap (:83-96) and kni_set_bitmap (:98-123) need

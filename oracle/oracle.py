@@ -110,6 +110,29 @@ def ref_kni_bitmap(ports: str | None) -> np.ndarray:
     return bm
 
 
+def ref_ini_events(path: str):
+    """(events, error) of the reference's own INI reader (inih, fs/lib/
+    ff_ini_parser.c compiled by build_ref.sh) over a file, recording every
+    (section, name, value) it hands the handler; None if oracle/_ref is absent."""
+    lib_path = HERE / "_ref" / "libref_ini.so"
+    if not lib_path.exists():
+        return None
+    R = ctypes.CDLL(str(lib_path))
+    H = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p,
+                         ctypes.c_char_p)
+    ev = []
+
+    def rec(_user, s, n, v):
+        ev.append((s.decode("latin-1"), n.decode("latin-1"), v.decode("latin-1")))
+        return 1
+
+    cb = H(rec)
+    R.ini_parse.restype = ctypes.c_int
+    R.ini_parse.argtypes = [ctypes.c_char_p, H, ctypes.c_void_p]
+    err = R.ini_parse(str(path).encode(), cb, None)
+    return ev, err
+
+
 def ref():
     """The reference's compiled toeplitz_hash, or None if oracle/_ref is absent."""
     global _ref

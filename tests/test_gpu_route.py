@@ -157,3 +157,28 @@ def test_route_burst_vs_process_packets(oracle_mod, queue_id, kni, cap, n):
     assert res.n_freed == len(freed_ref)
     assert res.n_unresolved == sum(1 for o in local_ref if f_ref[o[1]] in (-2, -3))
     assert [res.n_ring[j] for j in range(nq)] == [len(rings_ref[j]) for j in range(nq)]
+
+
+def test_from_ff_config_kni(oracle_mod, tmp_path):
+    """[kni] keys read from an fs/lib INI (ff_config.c:442-449) configure the
+    fused filter exactly as init_kni would (ff_dpdk_if.c:598-606)."""
+    ini = tmp_path / "kni.ini"
+    ini.write_text("[dpdk]\nlcore_mask=f\nsoft_dispatch=1\nport_list=0\n[system]\n"
+                   "dispatch_only_core=1\n[kni]\nenable=1\nmethod=accept\n"
+                   "tcp_port=80,443,8000-8080\nudp_port=53 ; dns\n[port0]\naddr=10.0.0.2\n"
+                   "netmask=255.255.255.0\nbroadcast=10.0.0.255\ngateway=10.0.0.1\n"
+                   "lcore_list=0-3\n")
+    n, stride = 30001, 80
+    with SoftRss.from_ff_config(str(ini), device=0, max_burst=0) as eng:
+        assert (eng.cfg.nb_procs, eng.nb_queues) == (4, 4)
+        win, lens = eng.synth(abi.SYN_FUZZ, n, 5, stride=stride)
+        res = eng.dispatch_dev(win, lens, stride, n, want_filter=True)
+        torch.cuda.synchronize()
+        w_h = win[: n * stride].cpu().numpy()
+        l_h = to_np(lens[:n], np.uint16)
+        want = oracle_mod.filter_windows(w_h, stride, l_h, True,
+                                         oracle_mod.kni_bitmap("80,443,8000-8080"),
+                                         oracle_mod.kni_bitmap("53"))
+        assert np.array_equal(res.filter[:n].cpu().numpy(), want)
+        q_ref, _ = oracle_mod.dispatch_windows(w_h, stride, l_h, oracle_mod.cfg(4, 4, 1, 1))
+        assert np.array_equal(to_np(res.q[:n], np.int16), q_ref)

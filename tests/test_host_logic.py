@@ -17,7 +17,17 @@ port_list=0,1
 [system]
 dispatch_only_core=1
 
+[port0]
+addr=10.0.0.2
+netmask=255.255.255.0
+broadcast=10.0.0.255
+gateway=10.0.0.1
+
 [port1]
+addr=10.0.1.2
+netmask=255.255.255.0
+broadcast=10.0.1.255
+gateway=10.0.1.1
 lcore_list=0-1
 """
 

@@ -113,9 +113,13 @@ class SoftRss:
         from .ffconfig import load_ff_config
 
         fc = load_ff_config(path)
-        return cls(nb_procs=fc.nb_procs, nb_queues=fc.nb_queues[port],
-                   soft_dispatch=fc.soft_dispatch,
-                   dispatch_only_core=fc.dispatch_only_core, device=device, **kw)
+        eng = cls(nb_procs=fc.nb_procs, nb_queues=fc.nb_queues[port],
+                  soft_dispatch=fc.soft_dispatch,
+                  dispatch_only_core=fc.dispatch_only_core, device=device, **kw)
+        if fc.kni_enable:
+            # init_kni (ff_dpdk_if.c:598-606) behind enable_kni (:921-923)
+            eng.set_kni(True, fc.kni_method, fc.kni_tcp_port, fc.kni_udp_port)
+        return eng
 
     # -- lifetime ---------------------------------------------------------
     def close(self) -> None:
