@@ -64,8 +64,8 @@ def parse_args(argv=None):
                     help="parse+hash only (no per-queue lists)")
     ap.add_argument("--filter", action="store_true",
                     help="also run the fused KNI protocol_filter (1 B/pkt more)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0,
-                    help="target CPU-baseline duration (0 disables)")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0,
+                    help="target CPU-baseline duration over its 8 cells (0 disables)")
     ap.add_argument("--pcie", type=int, default=1,
                     help="also time the host-resident (PCIe-inclusive) paths with "
                          "tools/yrss_cbench at N=1 (reported beside value, never as value)")
@@ -200,20 +200,73 @@ def sum_over_ranks(x: float, world: int) -> float:
 
 
 # ---- CPU baseline (oracle, rank 0 at N=1 only) ------------------------------------
-def cpu_baseline(args, nb_queues):
+CPU_PROFILES = ("udp4", "tcp4")        # the headline stream, and every packet hashed
+CPU_VARIANTS = ("bit_serial", "table")  # toeplitz_hash as written; 12x256 byte tables
+
+
+def cpu_worker(spec: str) -> int:
+    """One pinned CPU-baseline process (bench.py --cpu-worker prof:variant:secs:cpu):
+    the oracle's toeplitz_dispatch restatement over 2^20 packets of the stream,
+    one call per packet, repeated for about `secs` after a start line on stdin."""
+    prof, variant, secs, cpu = spec.split(":")
+    if cpu != "-":
+        os.sched_setaffinity(0, {int(cpu)})     # what taskset -c does
     from oracle import oracle
 
     n = 1 << 20
-    win, lens = oracle.synth(PROFILES[args.profile], n, 0, SEED, NFLOWS[args.profile],
-                             args.stride)
-    c = oracle.cfg(args.nb_procs, nb_queues, 1, args.dispatch_only_core)
+    win, lens = oracle.synth(PROFILES[prof], n, 0, SEED, NFLOWS[prof], 64)
+    c = oracle.cfg(3, 3, 1, 1)                  # fs/config/config.ini knobs
+    fast = variant == "table"
     t0 = time.perf_counter()
-    oracle.bench_dispatch(win, args.stride, lens, c, 1)
-    one = time.perf_counter() - t0
-    reps = max(1, int(args.cpu_seconds / max(one, 1e-6)))
+    oracle.bench_dispatch(win, 64, lens, c, 1, fast)
+    reps = max(1, int(float(secs) / max(time.perf_counter() - t0, 1e-6)))
+    print("ready", flush=True)
+    sys.stdin.readline()
     t0 = time.perf_counter()
-    oracle.bench_dispatch(win, args.stride, lens, c, reps)
-    dt = time.perf_counter() - t0
+    oracle.bench_dispatch(win, 64, lens, c, reps, fast)
+    print(json.dumps({"pkts": reps * n, "secs": time.perf_counter() - t0}), flush=True)
+    return 0
+
+
+def _cpu_run(prof: str, variant: str, secs: float, cpus) -> float:
+    """Mpkt/s of len(cpus) pinned worker processes started together."""
+    import subprocess
+
+    procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--cpu-worker",
+                               f"{prof}:{variant}:{secs}:{cpu}"],
+                              stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+             for cpu in cpus]
+    try:
+        for p in procs:
+            if p.stdout.readline().strip() != "ready":
+                raise RuntimeError("cpu worker failed to start")
+        for p in procs:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+        res = [json.loads(p.stdout.readline()) for p in procs]
+    finally:
+        for p in procs:
+            p.wait(timeout=600)
+    return sum(r["pkts"] for r in res) / max(r["secs"] for r in res) / 1e6
+
+
+def cpu_baseline(args, nb_queues):
+    """the reference's algorithm on the GPU box's host cores.
+    Both ports (bit-serial as the reference writes toeplitz_hash, and
+    table-driven), on the headline UDP stream and all-TCP, on 1 core (the
+    reference's single dispatching lcore, ff_dpdk_if.c:1653) and on every core
+    this job may use (at most 16: one GPU's share of the box), as independent
+    processes pinned one per core.  `value` is the bit-serial port on 1 core
+    over the bench's own stream."""
+    cpus = sorted(os.sched_getaffinity(0))
+    cpus_all = cpus[: max(1, min(16, len(cpus)))]
+    secs = max(0.5, args.cpu_seconds / (2 * len(CPU_PROFILES) * len(CPU_VARIANTS)))
+    by = {}
+    for prof in CPU_PROFILES:
+        by[prof] = {}
+        for var in CPU_VARIANTS:
+            by[prof][var] = {"1": round(_cpu_run(prof, var, secs, cpus_all[:1]), 2),
+                             str(len(cpus_all)): round(_cpu_run(prof, var, secs, cpus_all), 2)}
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -222,33 +275,16 @@ def cpu_baseline(args, nb_queues):
                 break
     except OSError:
         pass
-    out = {
-        "value": round(reps * n / dt / 1e6, 3), "unit": "Mpkt/s", "cores": 1, "kind": "port",
-        "sample": f"{reps} passes x {n} pkts of the same {args.profile} stream "
-                  f"({dt:.1f}s); bit-serial toeplitz_dispatch restatement, one call per "
-                  f"packet, gcc -O2 fs/lib flags; host CPU: {cpu}",
+    head = args.profile if args.profile in by else "udp4"
+    return {
+        "value": by[head]["bit_serial"]["1"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
+        "sample": f"2^20 packets of each stream re-run for ~{secs:.1f}s per cell, one "
+                  "toeplitz_dispatch call per packet (oracle restatement, gcc -O2 fs/lib "
+                  f"flags), processes pinned one per core; host CPU: {cpu}",
+        "all_cores": {"value": by[head]["bit_serial"][str(len(cpus_all))], "unit": "Mpkt/s",
+                      "cores": len(cpus_all)},
+        "by_profile": by,
     }
-    # also every host core this job may use, as independent workers
-    # (ctypes drops the GIL inside the C loop, so threads run in parallel).  The
-    # GPU box grants one GPU's share of the host: at most 16 cores.
-    from concurrent.futures import ThreadPoolExecutor
-
-    ncores = max(1, min(16, len(os.sched_getaffinity(0))))
-    reps_all = max(1, reps // 2)
-    copies = [win.copy() for _ in range(ncores)]
-
-    def work(i):
-        oracle.bench_dispatch(copies[i], args.stride, lens, c, reps_all)
-
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(ncores) as ex:
-        list(ex.map(work, range(ncores)))
-    dt_all = time.perf_counter() - t0
-    out["all_cores"] = {
-        "value": round(ncores * reps_all * n / dt_all / 1e6, 3), "unit": "Mpkt/s",
-        "cores": ncores,
-        "sample": f"{ncores} threads x {reps_all} passes x {n} pkts ({dt_all:.1f}s)"}
-    return out
 
 
 def probe_traffic(batches, n, stride, steps):
@@ -439,8 +475,21 @@ def main(argv=None):
     barrier(world)
     elapsed = max_over_ranks(t1 - t0, world)
     k_ms, k_cnt = eng.timing_read(abi.K_PARSE_HASH)
-    eng.timing_enable(0)
     k_avg_s = max_over_ranks(k_ms / max(k_cnt, 1) / 1e3, world)
+    eng.timing_enable(0)
+    # the scan and scatter shares, from a separate pass after the timed one:
+    # events on all three kernels widen the step by ~9 us, so the timed steps
+    # carry them on the parse kernel only
+    side_us = {}
+    if not args.no_compact and args.kernel_timing:
+        eng.timing_enable((1 << abi.K_SCAN) | (1 << abi.K_SCATTER))
+        for _ in range(min(args.steps, 20)):
+            step()
+        torch.cuda.synchronize()
+        for name, k in (("scan", abi.K_SCAN), ("scatter", abi.K_SCATTER)):
+            ms, cnt = eng.timing_read(k)
+            side_us[name] = round(max_over_ranks(ms / max(cnt, 1) / 1e3, world) * 1e6, 2)
+        eng.timing_enable(0)
 
     total_pkts = sum_over_ranks(float(n * args.steps), world)
     value = total_pkts / elapsed / 1e6
@@ -449,6 +498,14 @@ def main(argv=None):
     # queue (2) written = 72 B at 64-B windows.
     bpp = min(args.stride, 64) + 2 + 4 + 2 + (1 if args.filter else 0)
     achieved = bpp * n / k_avg_s / 1e9 if k_avg_s > 0 else 0.0
+    # the whole step: the same bytes plus the per-queue index lists (4 B/pkt
+    # written, SURVEY §8(d): "report B=76 in that mode") over ms_per_step
+    step_s = elapsed / args.steps
+    step_bpp = bpp + (0 if args.no_compact else 4)
+    step = {"bytes_per_pkt": step_bpp, "achieved": round(step_bpp * n / step_s / 1e9, 1),
+            "frac": round(step_bpp * n / step_s / 1e9 / HBM_PEAK_GBS, 4),
+            "parse_us": round(k_avg_s * 1e6, 2), **{f"{k}_us": v for k, v in side_us.items()},
+            "outside_parse_us": round((step_s - k_avg_s) * 1e6, 2)}
     key = {"profile": args.profile, "pkts": n, "stride": args.stride,
            "compact": not args.no_compact}
     traffic = load_traffic(args.pmc, key)
@@ -510,6 +567,7 @@ def main(argv=None):
                 "traffic": traffic,
                 "kernel": "yrss_parse_hash", "bytes_per_pkt": bpp,
                 "kernel_avg_us": round(k_avg_s * 1e6, 2),
+                "step": step,
                 "probe": None if probe_s is None else {
                     "what": "ideal-traffic twin (tools/yrss_probe.hip): same bytes, no parse",
                     "us": round(probe_s * 1e6, 2),
@@ -529,4 +587,6 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-worker":
+        sys.exit(cpu_worker(sys.argv[2]))
     sys.exit(main() or 0)
