@@ -1,10 +1,9 @@
 #!/usr/bin/env python3
 """Latency of a 2^24-packet device batch on context B while context A's
-persistent worker (128 workgroups, idle exit 3 s) is resident, with the
-device-wide yield (default) or without it (YRSS_NO_YIELD=1 in the env).
---filter runs B's batch through the KNI-filter parse kernel, whose LDS (94 KB)
-cannot share a CU with a worker workgroup (117 KB) nor fit twice on a free
-one: half its workgroups then wait for the worker's CUs."""
+persistent worker (128 workgroups, idle exit 3 s) is resident, and the
+latency of A's next burst.  --filter runs B's batch through the KNI-filter
+parse kernel (the largest LDS footprint).  The commit that built a device-wide
+yield read YRSS_NO_YIELD for its A/B (profiles/r02_v4_worker_yield_ab.log)."""
 import os
 import sys
 import time
@@ -47,6 +46,6 @@ with SoftRss(3, 3, 1, 1, device=0, max_burst=0) as b, SoftRss(3, 3, 1, 1, device
     relaunch = (time.perf_counter() - t0) * 1e3
     a.worker_stop()
     a.unregister_host_memory(pool.ctypes.data)
-print(f"yield={'off' if os.environ.get('YRSS_NO_YIELD') else 'on'} filter={int(filt)} "
+print(f"filter={int(filt)} "
       f"solo_ms={solo:.3f} "
       f"with_worker_ms={shared:.3f} next_burst_ms={relaunch:.3f}", flush=True)

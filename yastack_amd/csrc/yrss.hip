@@ -37,10 +37,6 @@
 #include <strings.h>
 #include <time.h>
 
-#include <fcntl.h>
-#include <sys/mman.h>
-#include <unistd.h>
-
 #include <map>
 #include <mutex>
 #include <vector>
@@ -1682,8 +1678,6 @@ struct WorkerParams {
     uint16_t *len;       // device scratch [nblocks][kWorkerMaxBurst]
     uint64_t *next;      // host-coherent [nblocks]: ticket to serve next (resume)
     WorkerCtl *wctl;     // host-coherent launch control
-    const uint64_t *yield;   // device-wide yield epoch (host-coherent, shared), or null
-    uint64_t yield_seen;     // its value at launch: any change means leave
     uint32_t nslots;
     uint64_t idle_ticks; // s_memrealtime ticks (100 MHz)
     uint64_t life_ticks;
@@ -1718,9 +1712,6 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
     const uint64_t t_begin = wall_clock64();
     uint64_t t_last = t_begin;
     uint64_t pub_seen = 0;   // thread 0 only: ring activity at the last idle check
-    uint32_t polls = 0;      // thread 0 only
-    bool yielded = false;    // thread 0 only: the yield epoch moved during a burst
-    uint64_t yv = W.yield_seen;
     if (threadIdx.x == 0)
         pub_seen = __hip_atomic_load(&W.wctl->pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     for (;;) {
@@ -1729,10 +1720,6 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         if (threadIdx.x == 0) {
             uint32_t go = 0;   // 1: a burst, 2: leave
             for (;;) {
-                if (yielded) {   // seen while busy, after the previous burst
-                    go = 2;
-                    break;
-                }
                 // seq, n and flags in one 16-byte read: the host writes n and
                 // flags before seq, so a new seq comes with its n and flags
                 const u32x4 hd = *reinterpret_cast<const volatile u32x4 *>(sl);
@@ -1746,14 +1733,6 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
                 if (__hip_atomic_load(&W.wctl->stop, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_SYSTEM) ||
                     now - t_begin > W.life_ticks) {
-                    go = 2;
-                    break;
-                }
-                // a full-device batch from any context or process bumped the
-                // device's yield epoch: give the CUs back (every 4th poll)
-                if (W.yield && (++polls & 3u) == 0u &&
-                    __hip_atomic_load(W.yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) !=
-                        W.yield_seen) {
                     go = 2;
                     break;
                 }
@@ -1777,10 +1756,6 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
                     __builtin_amdgcn_s_sleep(2);
             }
             if (go == 1) {
-                // a busy workgroup never polls: the yield word is read once per
-                // burst too, its PCIe round trip hidden behind the burst
-                if (W.yield)
-                    yv = __hip_atomic_load(W.yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                 __hip_atomic_store(W.fault + blockIdx.x, 0u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -1853,7 +1828,6 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
                                                  __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(W.done + si, t | (f ? kWorkerFault : 0ull), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
-            yielded = yv != W.yield_seen;
         }
         t_last = wall_clock64();
         t += gridDim.x;
@@ -1931,13 +1905,6 @@ struct PendingBurst {
     bool scan_fault = false;         // multi-kernel path: scan look-back fault
     uint64_t done_seq = 0;           // one-launch path: value the kernel stores in *h_done
     void *const *wb_mbufs = nullptr; // host-side hash.rss write-back (staged path)
-};
-
-// The device-wide yield page (see yield_attach).
-struct alignas(64) yrss_yield_page {
-    uint64_t epoch;            // bumped by a full-grid batch while workers exist
-    uint64_t busy_until_ns;    // CLOCK_MONOTONIC: workers relaunch after this
-    uint32_t workers;          // worker contexts on the device (all processes)
 };
 
 struct yrss_ctx {
@@ -2018,8 +1985,6 @@ struct yrss_ctx {
     uint32_t *dh_fault = nullptr;
     PendingBurst pend;
     // persistent burst worker (yrss_worker_*)
-    yrss_yield_page *yield = nullptr;          // the device's yield page (shared), or null
-    uint64_t *d_yield_epoch = nullptr;   // its epoch word, device view
     struct WorkerState {
         bool on = false;           // yrss_worker_start called
         bool running = false;      // a worker launch may still be in flight
@@ -2367,88 +2332,6 @@ uint64_t mono_ns()
 // context is never torn down under a running shim call.
 yrss_ctx *g_dispatch_ctx = nullptr;
 std::mutex g_dispatch_mu;
-
-// Device-wide yield.  A persistent worker (yrss_worker_*) keeps up to 128
-// workgroups resident, and a full-grid batch (the parse kernel puts one
-// workgroup on every CU) cannot share those CUs (LDS and VGPRs), so it would
-// wait for the worker's idle or lifetime exit (up to 1 s).  Every context of
-// every process on a device shares one page, named after the device's PCI
-// address in POSIX shared memory and mapped into the GPU: a full-grid batch
-// bumps `epoch` when workers exist, every worker workgroup that sees the
-// epoch move leaves between bursts (published tickets stay in the ring), and
-// no worker relaunches before `busy_until_ns`, the batch's expected end.
-struct DevYield {
-    yrss_yield_page *page = nullptr;
-    uint64_t *d_epoch = nullptr;
-    bool tried = false;
-};
-std::mutex g_yield_mu;
-std::map<int, DevYield> g_yield;
-
-// The device's page, created or attached once per process (null if neither
-// shared nor process-local pinned memory could be mapped into the GPU).
-yrss_yield_page *yield_attach(int device, uint64_t **d_epoch)
-{
-    std::lock_guard<std::mutex> lk(g_yield_mu);
-    DevYield &y = g_yield[device];
-    if (!y.tried) {
-        y.tried = true;
-        char bus[64] = {0};
-        void *m = MAP_FAILED;
-        if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus) - 1, device) == hipSuccess) {
-            char name[96];
-            snprintf(name, sizeof(name), "/yrss-yield-%s", bus);
-            for (char *q = name + 1; *q; ++q)
-                if (*q == ':' || *q == '/')
-                    *q = '_';
-            const int fd = shm_open(name, O_RDWR | O_CREAT, 0600);
-            if (fd >= 0) {
-                if (ftruncate(fd, 4096) == 0)
-                    m = mmap(nullptr, 4096, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-                close(fd);
-            }
-        }
-        void *d = nullptr;
-        if (m != MAP_FAILED) {
-            if (hipHostRegister(m, 4096, hipHostRegisterMapped) == hipSuccess &&
-                hipHostGetDevicePointer(&d, m, 0) == hipSuccess) {
-                y.page = static_cast<yrss_yield_page *>(m);
-            } else {
-                (void)hipGetLastError();
-                munmap(m, 4096);
-            }
-        }
-        if (!y.page) {
-            // this process's contexts still yield to each other
-            if (hipHostMalloc(&m, 4096, hipHostMallocMapped | hipHostMallocCoherent) ==
-                    hipSuccess &&
-                hipHostGetDevicePointer(&d, m, 0) == hipSuccess) {
-                memset(m, 0, 4096);
-                y.page = static_cast<yrss_yield_page *>(m);
-            } else {
-                (void)hipGetLastError();
-            }
-        }
-        y.d_epoch = y.page ? static_cast<uint64_t *>(d) : nullptr;
-    }
-    *d_epoch = y.d_epoch;
-    return y.page;
-}
-
-// Before a full-grid launch: make every worker on the device give its CUs
-// back for about the batch's duration (~40 Gpkt/s, plus 0.2 ms).
-void yield_device(yrss_ctx *c, uint32_t n)
-{
-    yrss_yield_page *y = c->yield;
-    if (!y || __atomic_load_n(&y->workers, __ATOMIC_ACQUIRE) == 0)
-        return;
-    const uint64_t until = mono_ns() + 200000ull + (uint64_t)n / 40u;
-    uint64_t cur = __atomic_load_n(&y->busy_until_ns, __ATOMIC_RELAXED);
-    while (cur < until && !__atomic_compare_exchange_n(&y->busy_until_ns, &cur, until, true,
-                                                       __ATOMIC_ACQ_REL, __ATOMIC_RELAXED)) {
-    }
-    __atomic_fetch_add(&y->epoch, 1ull, __ATOMIC_RELEASE);
-}
 
 // A scan look-back that never resolved leaves that batch's lists invalid.
 bool take_scan_fault(yrss_ctx *c)
@@ -2837,8 +2720,6 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         yrss_fini(c);
         return rc;
     }
-    if (!getenv("YRSS_NO_YIELD"))   // A/B switch (tools/gpu_yield_ab.sh)
-        c->yield = yield_attach(c->device, &c->d_yield_epoch);
     *out = c;
     return 0;
 }
@@ -3001,7 +2882,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         c->rank_cap = n;
     }
 
-    yield_device(c, n);   // other contexts' and processes' workers leave the CUs
     ParseParams P = c->proto;
     P.win = b->win;
     P.len = b->len;
@@ -3621,8 +3501,6 @@ namespace {
 void worker_free(yrss_ctx *c)
 {
     auto &w = c->w;
-    if (w.on && c->yield)
-        __atomic_fetch_sub(&c->yield->workers, 1u, __ATOMIC_ACQ_REL);
     (void)hipHostFree(w.slots);
     (void)hipHostFree(w.done);
     (void)hipFree(w.fault);
@@ -3687,8 +3565,6 @@ int worker_launch(yrss_ctx *c)
     W.idle_ticks = w.idle_ticks;
     W.life_ticks = w.life_ticks;
     W.poll_sleep = w.poll_sleep;
-    W.yield = c->d_yield_epoch;
-    W.yield_seen = c->yield ? __atomic_load_n(&c->yield->epoch, __ATOMIC_ACQUIRE) : 0u;
     hipLaunchKernelGGL(yrss_burst_worker, dim3(w.nblocks), dim3(kSmallBlock),
                        worker_lds(c->nb), w.stream, W);
     YRSS_HIP(hipGetLastError());
@@ -3708,12 +3584,7 @@ int worker_ensure(yrss_ctx *c)
         return 0;
     YRSS_HIP(hipSetDevice(c->device));
     const int rc = worker_halt(c);
-    if (rc)
-        return rc;
-    // a full-grid batch holds the device: relaunch on a later submit or poll
-    if (c->yield && mono_ns() < __atomic_load_n(&c->yield->busy_until_ns, __ATOMIC_ACQUIRE))
-        return 0;
-    return worker_launch(c);
+    return rc ? rc : worker_launch(c);
 }
 
 }  // namespace
@@ -3792,8 +3663,6 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
         w.out[i] = yrss_ctx::WorkerState::Out{nullptr, nullptr, nullptr, nullptr, 0u, true, 0u};
     w.issued = 0;
     w.on = true;
-    if (c->yield)
-        __atomic_fetch_add(&c->yield->workers, 1u, __ATOMIC_ACQ_REL);
     return 0;
 }
 
