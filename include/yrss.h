@@ -453,6 +453,43 @@ int yrss_worker_poll(yrss_ctx *ctx, uint64_t ticket, int wait);
 /* Stop the kernel and free the ring (also done by yrss_fini). */
 int yrss_worker_stop(yrss_ctx *ctx);
 
+/* ---- host bursts fanned out over several GPUs ------------------- */
+
+/* The reference's soft dispatch is ONE lcore feeding every dispatch ring
+ * (fs/lib/ff_dpdk_if.c:1653-1683).  A fan-out keeps that single dispatcher
+ * thread and spreads its consecutive bursts round-robin over nctx contexts,
+ * each with its own persistent worker (yrss_worker_*) on its own device and
+ * PCIe link: burst g (tickets 1, 2, ...) goes to context (g - 1) % nctx.
+ * yrss_fanout_next returns tickets in submission order as they complete, so
+ * handing each burst's per-queue lists to the rings in that order keeps every
+ * queue FIFO over the whole stream, as rte_ring does (:1087-1093).  devices may
+ * repeat (several contexts on one GPU).  Host memory is registered with every
+ * context.  Submit and next come from one thread (the dispatcher lcore); each
+ * context holds up to nslots bursts, and a ticket must be returned by
+ * yrss_fanout_next before its context's slot is reused (submit: -EBUSY). */
+#define YRSS_FANOUT_MAX_CTX 64
+typedef struct yrss_fanout yrss_fanout;
+int yrss_fanout_init(const struct yrss_config *cfg, const int *devices, uint32_t nctx,
+                     uint32_t nslots, uint32_t nblocks, yrss_fanout **out);
+int yrss_fanout_fini(yrss_fanout *f);
+uint32_t yrss_fanout_size(yrss_fanout *f);
+int yrss_fanout_register_host_memory(yrss_fanout *f, void *base, size_t len);
+int yrss_fanout_unregister_host_memory(yrss_fanout *f, void *base);
+/* As yrss_worker_submit / yrss_worker_submit_frames; *ticket is the fan-out's. */
+int yrss_fanout_submit(yrss_fanout *f, void *const *mbufs, uint32_t n, int16_t *out_q,
+                       uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                       uint32_t flags, uint64_t *ticket);
+int yrss_fanout_submit_frames(yrss_fanout *f, const uint8_t *const *data, const uint16_t *len,
+                              uint32_t n, int16_t *out_q, uint32_t *out_hash,
+                              uint32_t *out_qidx, uint32_t *out_qstart, uint64_t *ticket);
+/* The oldest ticket not yet returned, once its burst is done: 0 with *ticket
+ * set (-EFAULT also sets it: the burst is consumed, a pointer was outside every
+ * registered range); -EAGAIN: still running (wait = 0); -ENOENT: nothing
+ * outstanding; other errors as yrss_worker_poll. */
+int yrss_fanout_next(yrss_fanout *f, int wait, uint64_t *ticket);
+/* Host-only: the context serving fan-out ticket `ticket`, and its ticket there. */
+int yrss_fanout_route(uint64_t ticket, uint32_t nctx, uint32_t *ctx, uint64_t *ctx_ticket);
+
 /* ---- device-side status ----------------------------------------------------------- */
 
 /* Synchronises the device and reports (then clears) a device-side fault of an

@@ -8,10 +8,10 @@ tests and ``bench.py``; C hosts (F-Stack itself) link the library directly
 """
 from . import abi
 from .abi import YrssError, YrssLibraryError
-from .dispatch import DispatchResult, SoftRss
+from .dispatch import DispatchResult, FanOut, SoftRss
 from .shard import merge_queue_lists, shard_range
 
 __all__ = [
-    "abi", "SoftRss", "DispatchResult", "YrssError", "YrssLibraryError",
+    "abi", "SoftRss", "FanOut", "DispatchResult", "YrssError", "YrssLibraryError",
     "shard_range", "merge_queue_lists",
 ]

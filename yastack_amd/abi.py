@@ -162,6 +162,19 @@ _PROTOS = {
                                         ctypes.POINTER(ctypes.c_uint64),
                                         ctypes.POINTER(ctypes.c_uint64)]),
     "yrss_merge_queue_lists": (ctypes.c_int, [_u32, _u32, _vp, _vp, _vp, _vp, _vp]),
+    "yrss_fanout_init": (ctypes.c_int, [ctypes.POINTER(Config), _vp, _u32, _u32, _u32,
+                                        ctypes.POINTER(_vp)]),
+    "yrss_fanout_fini": (ctypes.c_int, [_vp]),
+    "yrss_fanout_size": (_u32, [_vp]),
+    "yrss_fanout_register_host_memory": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    "yrss_fanout_unregister_host_memory": (ctypes.c_int, [_vp, _vp]),
+    "yrss_fanout_submit": (ctypes.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32,
+                                          ctypes.POINTER(ctypes.c_uint64)]),
+    "yrss_fanout_submit_frames": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp,
+                                                 ctypes.POINTER(ctypes.c_uint64)]),
+    "yrss_fanout_next": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
+    "yrss_fanout_route": (ctypes.c_int, [ctypes.c_uint64, _u32, ctypes.POINTER(_u32),
+                                         ctypes.POINTER(ctypes.c_uint64)]),
     "yrss_set_dispatch_ctx": (ctypes.c_int, [_vp]),
     "yrss_toeplitz_dispatch": (ctypes.c_int, [_vp, ctypes.c_uint16, ctypes.c_uint16,
                                               ctypes.c_uint16]),

@@ -409,3 +409,87 @@ class SoftRss:
 
     def grid_for(self, n: int) -> int:
         return int(self._lib.yrss_grid_for(self._ctx, n))
+
+
+class FanOut:
+    """One dispatcher thread's host bursts spread round-robin over several
+    contexts / GPUs (``yrss_fanout_*``), returned in submission order by
+    :meth:`next` so per-queue FIFO holds over the whole stream."""
+
+    def __init__(self, devices, nb_procs: int = 3, nb_queues: int | None = None,
+                 soft_dispatch: int = 1, dispatch_only_core: int = 1, nslots: int = 16,
+                 nblocks: int = 4):
+        self._lib = abi.load()
+        cfg = abi.default_config()
+        cfg.nb_procs = nb_procs
+        cfg.nb_queues = nb_procs if nb_queues is None else nb_queues
+        cfg.soft_dispatch = soft_dispatch
+        cfg.dispatch_only_core = dispatch_only_core
+        self.nb_queues = int(cfg.nb_queues)
+        devs = (ctypes.c_int * len(devices))(*devices)
+        f = ctypes.c_void_p()
+        abi.check(self._lib.yrss_fanout_init(ctypes.byref(cfg), devs, len(devices), nslots,
+                                             nblocks, ctypes.byref(f)), "yrss_fanout_init")
+        self._f = f
+        self._res = {}
+
+    def close(self) -> None:
+        if getattr(self, "_f", None) and self._f.value:
+            rc = self._lib.yrss_fanout_fini(self._f)
+            self._f = ctypes.c_void_p()
+            abi.check(rc, "yrss_fanout_fini")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def register_host_memory(self, base: int, nbytes: int) -> None:
+        abi.check(self._lib.yrss_fanout_register_host_memory(self._f, base, nbytes),
+                  "yrss_fanout_register_host_memory")
+
+    def unregister_host_memory(self, base: int) -> None:
+        abi.check(self._lib.yrss_fanout_unregister_host_memory(self._f, base),
+                  "yrss_fanout_unregister_host_memory")
+
+    def _outs(self, n):
+        q = np.empty(max(n, 1), np.int16)
+        h = np.empty(max(n, 1), np.uint32)
+        qi = np.empty(max(n, 1), np.uint32)
+        qs = np.empty(self.nb_queues + 2, np.uint32)
+        return q, h, qi, qs
+
+    def submit(self, mbuf_ptrs: np.ndarray) -> int:
+        mb = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
+        n = int(mb.size)
+        q, h, qi, qs = self._outs(n)
+        t = ctypes.c_uint64()
+        abi.check(self._lib.yrss_fanout_submit(self._f, _ptr(mb), n, _ptr(q), _ptr(h), _ptr(qi),
+                                               _ptr(qs), 0, ctypes.byref(t)), "yrss_fanout_submit")
+        self._res[t.value] = DispatchResult(q[:n], h[:n], qi[:n], qs)
+        return t.value
+
+    def submit_frames(self, data_ptrs: np.ndarray, lens: np.ndarray) -> int:
+        dp = np.ascontiguousarray(data_ptrs, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint16)
+        n = int(dp.size)
+        q, h, qi, qs = self._outs(n)
+        t = ctypes.c_uint64()
+        abi.check(self._lib.yrss_fanout_submit_frames(self._f, _ptr(dp), _ptr(ln), n, _ptr(q),
+                                                      _ptr(h), _ptr(qi), _ptr(qs),
+                                                      ctypes.byref(t)),
+                  "yrss_fanout_submit_frames")
+        self._res[t.value] = DispatchResult(q[:n], h[:n], qi[:n], qs)
+        return t.value
+
+    def next(self, wait: bool = True):
+        """(ticket, DispatchResult) of the oldest outstanding burst once done;
+        None while it runs (wait=False) or when nothing is outstanding."""
+        t = ctypes.c_uint64()
+        rc = self._lib.yrss_fanout_next(self._f, 1 if wait else 0, ctypes.byref(t))
+        if rc in (-11, -2):   # -EAGAIN, -ENOENT
+            return None
+        res = self._res.pop(t.value, None) if rc in (0, -14) else None
+        abi.check(rc, "yrss_fanout_next")
+        return t.value, res
