@@ -368,6 +368,40 @@ def pcie_inclusive(profile: str):
     return out or None
 
 
+def pcie_fanout(profile: str, world: int):
+    """Host-resident rate of ONE dispatcher thread fanning its bursts out over
+    all `world` GPUs (yrss_fanout_*, tools/yrss_cbench mode 5): the reference's
+    single dispatching lcore (ff_dpdk_if.c:1653) with N PCIe links behind it.
+    Run by rank 0 once every rank's device work is done."""
+    import subprocess
+
+    exe = ROOT / "tools" / "yrss_cbench"
+    if not exe.exists():
+        return None
+    out = []
+    one = bool(os.environ.get("YRSS_BENCH_ONE_DEVICE"))   # rehearsal: N contexts, device 0
+    devs = ",".join("0" if one else str(d) for d in range(world))
+    for frames, burst, blocks in (("1", 32, 128), ("1", 1024, 32), ("0", 32, 128)):
+        try:
+            r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
+                               capture_output=True, text=True, timeout=240,
+                               env={**os.environ, "YRSS_CBENCH_MODES": "5",
+                                    "YRSS_CBENCH_FANOUT_DEVICES": devs,
+                                    "YRSS_CBENCH_WORKER_DEPTH": str(4 * blocks),
+                                    "YRSS_CBENCH_WORKER_BLOCKS": str(blocks),
+                                    "YRSS_CBENCH_WORKER_FRAMES": frames})
+        except subprocess.TimeoutExpired:
+            break
+        for line in r.stdout.splitlines():
+            try:
+                d = json.loads(line)
+            except ValueError:
+                continue
+            out.append({"api": d["api"], "burst": d["burst"], "gpus": d["gpus"],
+                        "inflight": d["inflight"], "blocks": d["blocks"], "mpps": d["mpps"]})
+    return out or None
+
+
 def load_traffic(path: str, key: dict):
     """Per-launch HBM bytes for the parse kernel from a committed PMC summary
     of the same workload (profiles/pmc_parse_hash.json), else None."""
@@ -531,10 +565,15 @@ def main(argv=None):
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, nbq)
-    pcie = None
-    if rank == 0 and world == 1 and args.pcie:
-        eng.close()                       # release the device buffers first
-        pcie = pcie_inclusive(args.profile)
+    pcie = fan = None
+    if args.pcie:
+        barrier(world)                    # every rank's device work is done
+        if rank == 0:
+            eng.close()                   # release the device buffers first
+            if world == 1:
+                pcie = pcie_inclusive(args.profile)
+            fan = pcie_fanout(args.profile, world)
+        barrier(world)
 
     if rank == 0:
         line = {
@@ -576,6 +615,7 @@ def main(argv=None):
             },
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "pcie_fanout": fan,
             "check": check,
         }
         print(json.dumps(line), flush=True)

@@ -10,7 +10,9 @@
  * dispatcher loop of main_loop_vm_3 (fs/lib/ff_dpdk_if.c:1655-1683).
  *
  *   yrss_cbench [profile] [pool_pkts] [burst] [seconds]
- * prints one JSON line per burst size.
+ * prints one JSON line per burst size.  YRSS_CBENCH_MODES picks the paths:
+ * 0-3 the one-call burst APIs, 4 the persistent worker, 5 the multi-GPU
+ * fan-out (YRSS_CBENCH_FANOUT_DEVICES).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -146,6 +148,104 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
     fflush(stdout);
     free(tk);
     yrss_fini(ctx);
+    return 0;
+}
+
+/* Fan-out (yrss_fanout_*): one dispatcher thread, bursts round-robin over the
+ * contexts of YRSS_CBENCH_FANOUT_DEVICES (e.g. "0,1,2,3"; default "0"), each
+ * with its own worker (`depth` slots, `blocks` workgroups), handed back in
+ * submission order; the oldest is taken once every slot is busy. */
+static int run_fanout(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_sz,
+                      uint8_t *arena, size_t arena_sz, void **mbufs, uint32_t pool, uint32_t B,
+                      double secs, int16_t *q_all, uint32_t *h_all, uint32_t *qi_all,
+                      uint32_t profile, const uint8_t **fdata, uint16_t *flen)
+{
+    const char *fe = getenv("YRSS_CBENCH_WORKER_FRAMES");
+    const int frames = fe && atoi(fe) != 0;
+    if (frames)
+        fill_frames(mbufs, pool, fdata, flen);   /* outside the timed region */
+    const char *de = getenv("YRSS_CBENCH_WORKER_DEPTH");
+    const char *be = getenv("YRSS_CBENCH_WORKER_BLOCKS");
+    const char *dv = getenv("YRSS_CBENCH_FANOUT_DEVICES");
+    unsigned blocks = be ? (unsigned)atoi(be) : 32u;
+    unsigned depth = de ? (unsigned)atoi(de) : 4u * blocks;
+    if (blocks < 1 || blocks > YRSS_WORKER_MAX_BLOCKS)
+        blocks = 32;
+    depth = (depth < blocks ? blocks : depth + blocks - 1) / blocks * blocks;
+    int devs[YRSS_FANOUT_MAX_CTX];
+    unsigned nd = 0;
+    for (const char *p = dv ? dv : "0"; *p && nd < YRSS_FANOUT_MAX_CTX;) {
+        devs[nd++] = atoi(p);
+        while (*p && *p != ',')
+            ++p;
+        if (*p == ',')
+            ++p;
+    }
+    const uint64_t inflight = (uint64_t)nd * depth;
+    if (inflight * B > pool || B > YRSS_WORKER_MAX_BURST)
+        return 0;
+    yrss_fanout *f = NULL;
+    int rc;
+    if ((rc = yrss_fanout_init(cfg0, devs, nd, depth, blocks, &f)) ||
+        (rc = yrss_fanout_register_host_memory(f, mem, mem_sz)) ||
+        (rc = yrss_fanout_register_host_memory(f, arena, arena_sz))) {
+        fprintf(stderr, "fanout setup: %d\n", rc);
+        return 2;
+    }
+    uint32_t(*qs)[YRSS_MAX_QUEUES + 2] = calloc(inflight, sizeof(*qs));
+    uint64_t pkts = 0, issued = 0, handed = 0, t;
+    uint32_t off = 0;
+    double t0 = 0, t1 = 0;
+    for (int pass = 0; pass < 2; ++pass) {          /* pass 0: warm-up */
+        const double lim = pass ? secs : 0.2;
+        t0 = now();
+        t1 = t0;
+        pkts = 0;
+        while (t1 - t0 < lim) {
+            if (off + B > pool)
+                off = 0;
+            if (issued - handed == inflight) {
+                if ((rc = yrss_fanout_next(f, 1, &t)) != 0 || t != handed + 1) {
+                    fprintf(stderr, "fanout next: %d\n", rc);
+                    return 3;
+                }
+                ++handed;
+            }
+            const unsigned k = (unsigned)(issued % inflight);
+            rc = frames ? yrss_fanout_submit_frames(f, fdata + off, flen + off, B, q_all + off,
+                                                    h_all + off, qi_all + off, qs[k], &t)
+                        : yrss_fanout_submit(f, mbufs + off, B, q_all + off, h_all + off,
+                                             qi_all + off, qs[k], 0, &t);
+            if (rc != 0) {
+                fprintf(stderr, "fanout submit: %d\n", rc);
+                return 3;
+            }
+            ++issued;
+            off += B;
+            pkts += B;
+            if ((issued & 63u) == 0)
+                t1 = now();
+        }
+    }
+    while (handed < issued) {
+        if ((rc = yrss_fanout_next(f, 1, &t)) != 0) {
+            fprintf(stderr, "fanout next: %d\n", rc);
+            return 3;
+        }
+        ++handed;
+    }
+    t1 = now();
+    printf("{\"tool\": \"yrss_cbench\", \"api\": \"%s\", \"profile\": %u, "
+           "\"burst\": %u, \"gpus\": %u, \"inflight\": %llu, \"blocks\": %u, \"pkts\": %llu, "
+           "\"seconds\": %.3f, \"mpps\": %.2f, \"mode\": 5, \"note\": \"one dispatcher "
+           "thread, bursts round-robin over %u contexts' persistent workers, handed off in "
+           "submission order; %s read over PCIe\"}\n",
+           frames ? "yrss_fanout_submit_frames" : "yrss_fanout_submit", profile, B, nd,
+           (unsigned long long)inflight, blocks, (unsigned long long)pkts, t1 - t0,
+           pkts / (t1 - t0) / 1e6, nd, frames ? "windows" : "mbuf headers + windows");
+    fflush(stdout);
+    free(qs);
+    yrss_fanout_fini(f);
     return 0;
 }
 
@@ -317,6 +417,16 @@ int main(int argc, char **argv)
             const uint32_t B = burst_arg ? burst_arg : bursts[bi];
             const int rc = run_worker(&cfg, mem, mem_sz, arena, arena_sz, mbufs, pool, B, secs,
                                       q_all, h_all, qi_all, profile, thp, fdata, flen);
+            if (rc)
+                return rc;
+            if (burst_arg)
+                break;
+        }
+    if (mode_env && strchr(mode_env, '5'))
+        for (unsigned bi = 0; bi < 2; ++bi) {
+            const uint32_t B = burst_arg ? burst_arg : bursts[bi];
+            const int rc = run_fanout(&cfg, mem, mem_sz, arena, arena_sz, mbufs, pool, B, secs,
+                                      q_all, h_all, qi_all, profile, fdata, flen);
             if (rc)
                 return rc;
             if (burst_arg)
