@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
 #include <stdlib.h>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -53,6 +54,50 @@ __global__ __launch_bounds__(512) void rd_stride(const u32x4 *a, size_t nchunks,
     }
     if (x == 0x9E3779B9u)
         sink[0] = x;
+}
+
+// write-only: grid-stride 16-byte stores of an index pattern (the 1-bucket
+// scatter's list run), U stores per lane per step
+template <bool NT, int U>
+__global__ __launch_bounds__(512) void wr_stride(u32x4 *b, size_t nchunks, uint32_t base)
+{
+    const size_t T = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (U - 1) * T < nchunks; i += U * T) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t x = base + 4u * (uint32_t)(i + u * T);
+            const u32x4 v = {x, x + 1u, x + 2u, x + 3u};
+            if (NT)
+                __builtin_nontemporal_store(v, b + i + u * T);
+            else
+                b[i + u * T] = v;
+        }
+    }
+    for (; i < nchunks; i += T) {
+        const uint32_t x = base + 4u * (uint32_t)i;
+        const u32x4 v = {x, x + 1u, x + 2u, x + 3u};
+        if (NT)
+            __builtin_nontemporal_store(v, b + i);
+        else
+            b[i] = v;
+    }
+}
+
+// write-only, the scatter's shape: one wave per group of G 16-byte vectors
+// (G = 1024: a 4096-packet group's list), 1 KiB per wave-instruction
+template <int G>
+__global__ __launch_bounds__(256) void wr_group(u32x4 *b, size_t nchunks, uint32_t base)
+{
+    const size_t w = (size_t)blockIdx.x * 4 + threadIdx.x / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t v = lane; v < G; v += 64) {
+        const size_t i = w * G + v;
+        if (i < nchunks) {
+            const uint32_t x = base + 4u * (uint32_t)i;
+            __builtin_nontemporal_store(u32x4{x, x + 1u, x + 2u, x + 3u}, b + i);
+        }
+    }
 }
 
 // copy: read 16 B, write 16 B (the guide's float4 copy)
@@ -292,6 +337,29 @@ int main(int argc, char **argv)
                algo_bytes / us / 1e3, algo_bytes);
         fflush(stdout);
     };
+    if (argc > 2 && !strcmp(argv[2], "write")) {
+        // 4 rotating buffers of `sz` bytes (as the bench's 4 batches' lists)
+        for (size_t sz : {(size_t)64 << 20, bytes / 4}) {
+            const size_t nc = sz / 16;
+            int r = 0;
+            char nm[96];
+#define W(NT, U, grid, label)                                                                     \
+            snprintf(nm, sizeof nm, "write %s %zu MiB x4 rot", label, sz >> 20);                  \
+            rep(nm, (double)sz, time_us([&] { wr_stride<NT, U><<<(grid), 512>>>(b + (r++ % 4) * nc, nc, 7u); }, reps));
+            W(true, 1, (unsigned)cus, "nt U1 grid=1xCU")
+            W(true, 4, (unsigned)cus, "nt U4 grid=1xCU")
+            W(true, 1, (unsigned)cus * 2, "nt U1 grid=2xCU")
+            W(true, 1, (unsigned)cus * 4, "nt U1 grid=4xCU")
+            W(true, 1, (unsigned)(nc / 512), "nt U1 oneshot")
+            W(false, 1, (unsigned)cus, "dflt U1 grid=1xCU")
+            W(false, 1, (unsigned)(nc / 512), "dflt U1 oneshot")
+            W(true, 1, (unsigned)(nc / 2048), "nt U1 grid=n/4")
+#undef W
+            snprintf(nm, sizeof nm, "write nt wave-per-16KiB (scatter shape) %zu MiB x4 rot", sz >> 20);
+            rep(nm, (double)sz, time_us([&] { wr_group<1024><<<(unsigned)((nc / 1024 + 3) / 4), 256>>>(b + (r++ % 4) * nc, nc, 7u); }, reps));
+        }
+        return 0;
+    }
     rep("read nt U4 grid=1xCU", (double)bytes,
         time_us([&] { rd_stride<true, 4><<<cus, 512>>>(a, nchunks, sink); }, reps));
     rep("read nt U1 oneshot", (double)bytes,
