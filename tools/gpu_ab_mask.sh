@@ -1,4 +1,4 @@
-# A/B of the single-list short path (bucket-seen mask; default) against the
+# A/B of the single-list short path (bucket-seen mask; commit "Single-list short path (WIP"; removed after) against the
 # full scan + scatter (YRSS_NO_MASK=1), after the GPU parity suite.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp PYTHONUNBUFFERED=1

@@ -57,7 +57,6 @@ constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
 constexpr int kScatterRound = 8;       // packets per lane per scatter round
 constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this many buckets
 constexpr uint32_t kRankStage = 1024;   // ranked scatter: chunk stage (packets) per wave
-constexpr uint32_t kMaskWords = 16;     // bucket-seen mask: words per set (spreads the atomics)
 constexpr uint32_t kImgPkts = 4096;     // few-bucket scatter: largest group built in LDS
 constexpr uint32_t kImgLine = 32;       // entries per 128-byte line
 constexpr uint32_t kImgWords = kImgPkts + 8u * 2u * kImgLine;   // + up to 2 lines of slack per bucket
@@ -107,7 +106,6 @@ struct ParseParams {
     const uint32_t *kni_bm;   // tcp bitmap (2048 words) then udp bitmap (2048 words)
     uint32_t kni_enable;
     uint32_t out16;       // q/hash bursts as 16-byte stores: 1 plain, 2 sc1 (YRSS_OUT16)
-    unsigned long long *bmask;   // kCount == 1: OR of the buckets seen, [kMaskWords], or null
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
@@ -128,7 +126,6 @@ struct ScatterParams {
     uint32_t chunk;            // packets per chunk
     const uint16_t *rank;      // ranked mode: rank in chunk per packet (parse kCount == 2)
     uint32_t img;              // few-bucket groups assemble their lists in LDS (seg <= kImgPkts)
-    const unsigned long long *bmask;   // the parse kernel's bucket-seen mask, or null
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -650,32 +647,9 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     const uint32_t k = P.nchunk > gw ? (P.nchunk - gw + W - 1) / W : 0u;   // chunks owned
     if (kCount) {
         wave_lds_sync();
-        uint32_t seen = 0;
         for (uint32_t j = 0; j < k; ++j)
-            for (uint32_t b = lane; b < P.nb; b += kWave) {
-                const uint32_t v = cnt_w[j * P.nb + b];
-                P.seg_cnt[(size_t)b * P.ncol + gw + j * W] = v;
-                seen |= v;
-            }
-        if (kCount == 1 && P.bmask) {
-            // buckets this workgroup saw, one device atomic per workgroup into
-            // one of kMaskWords words: the scan and scatter kernels take a
-            // batch that feeds a single bucket (all-UDP traffic) on a short path
-            const uint64_t wm = P.nb <= (uint32_t)kWave ? __ballot(seen != 0u) : ~0ull;
-            unsigned long long *sh = reinterpret_cast<unsigned long long *>(
-                smem + kTblBytes);   // wave 0's staging tile, free once every wave is done
-            __syncthreads();
-            if (lane == 0)
-                sh[wave] = wm;
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                unsigned long long m = 0;
-                for (int w = 0; w < kWaves; ++w)
-                    m |= sh[w];
-                __hip_atomic_fetch_or(P.bmask + blockIdx.x % kMaskWords, m, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
+            for (uint32_t b = lane; b < P.nb; b += kWave)
+                P.seg_cnt[(size_t)b * P.ncol + gw + j * W] = cnt_w[j * P.nb + b];
     }
 }
 
@@ -712,9 +686,7 @@ struct ScanParams {
     uint32_t *totals;        // [nb]
     unsigned long long *status;   // [nb][tiles]: flag | epoch:31 | value:32
     uint32_t *fault;
-    const unsigned long long *bmask;   // this batch's bucket-seen mask, or null
-    unsigned long long *bmask_next;    // the next batch's, cleared here
-    uint32_t nchunk, ncol, tiles, epoch, n;
+    uint32_t nchunk, ncol, tiles, epoch;
 };
 
 __device__ __forceinline__ unsigned long long scan_status(uint32_t epoch, bool incl, uint32_t v)
@@ -722,33 +694,11 @@ __device__ __forceinline__ unsigned long long scan_status(uint32_t epoch, bool i
     return (incl ? kStFlagP : 0ull) | ((unsigned long long)(epoch & 0x7fffffffu) << 32) | v;
 }
 
-// The bucket-seen mask of a batch, read by every lane (kMaskWords words).
-__device__ __forceinline__ uint64_t batch_mask(const unsigned long long *bm, uint32_t lane)
-{
-    uint64_t m = lane < kMaskWords ? bm[lane] : 0ull;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1)   // across all 64 lanes: the result is wave-uniform
-        m |= (uint64_t)__shfl_xor((unsigned long long)m, d, kWave);
-    return m;
-}
-
 __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
 {
     __shared__ uint32_t wsum[kScanBlock / kWave];
     __shared__ uint32_t prefix_sh;
     const uint32_t b = blockIdx.x / P.tiles, p = blockIdx.x % P.tiles;
-    if (P.bmask) {
-        if (blockIdx.x == 0 && threadIdx.x < kMaskWords)
-            P.bmask_next[threadIdx.x] = 0ull;
-        // a batch that feeds one bucket needs no prefix: its list is the
-        // identity (the scatter writes it from the mask alone)
-        const uint64_t m = batch_mask(P.bmask, lane_id());
-        if (__popcll(m) == 1) {
-            if (p == 0 && threadIdx.x == 0)
-                P.totals[b] = ((m >> b) & 1ull) ? P.n : 0u;
-            return;
-        }
-    }
     const uint32_t lane = lane_id(), wave = threadIdx.x / kWave;
     const uint32_t col = p * kScanTile + threadIdx.x * 4u;
     const uint4 *row = reinterpret_cast<const uint4 *>(P.cnt + (size_t)b * P.ncol);
@@ -1056,34 +1006,6 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
 
     // start[b] = exclusive scan of totals; off[b] = start[b] + the prefix at
     // the group's first chunk; kseg = buckets this group feeds
-    if (P.bmask) {
-        const uint64_t m = batch_mask(P.bmask, lane);
-        if (__popcll(m) == 1) {
-            // every packet feeds bucket bk: qstart steps from 0 to n after bk,
-            // and the list is 0, 1, ..., n-1, written grid-stride as 16-byte
-            // non-temporal stores (the layout that writes fastest: 64 MB in
-            // 10.7 us against 11.9 for one group per wave, tools/hbm_bw.hip)
-            const uint32_t bk = (uint32_t)__builtin_ctzll(m);
-            if (gw == 0)
-                for (uint32_t k = lane; k <= P.nb; k += kWave)
-                    P.qstart[k] = k > bk ? P.n : 0u;
-            const uint32_t head = min(P.n, (4u - (uint32_t)(((uintptr_t)P.qidx >> 2) & 3u)) & 3u);
-            const uint32_t nv = (P.n - head) >> 2;
-            const uint32_t T = gridDim.x * blockDim.x;
-            const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
-            if (id < head)
-                P.qidx[id] = id;
-            u32x4 *dst = reinterpret_cast<u32x4 *>(P.qidx + head);
-            for (uint32_t v = id; v < nv; v += T) {
-                const uint32_t x = head + 4u * v;
-                __builtin_nontemporal_store(u32x4{x, x + 1u, x + 2u, x + 3u}, dst + v);
-            }
-            const uint32_t t = head + 4u * nv + id;
-            if (t < P.n)
-                P.qidx[t] = t;
-            return;
-        }
-    }
     const uint32_t col = gw << P.gshift, col_end = col + (1u << P.gshift);
     uint32_t carry = 0, kseg = 0;
     for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
@@ -2019,9 +1941,6 @@ struct yrss_ctx {
     uint32_t *d_seg_cnt = nullptr;
     uint32_t *d_seg_off = nullptr;
     uint32_t *d_totals = nullptr;
-    unsigned long long *d_bmask = nullptr;   // [2][kMaskWords] bucket-seen masks
-    uint32_t mask_par = 0;                   // set of the next single-list batch
-    bool no_mask = false;                    // YRSS_NO_MASK: no single-bucket short path
     // host-burst staging (pinned) and its device mirror
     hipStream_t stream = nullptr;
     uint32_t burst_cap = 0;
@@ -2726,8 +2645,6 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         c->no_rank = atoi(e) != 0;
     if (const char *e = getenv("YRSS_NO_IMG"))
         c->no_img = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_NO_MASK"))
-        c->no_mask = atoi(e) != 0;
     if (const char *e = getenv("YRSS_GROUP_TILES")) {
         const int v = atoi(e);
         if (v >= 1 && v <= 65536)
@@ -2769,10 +2686,6 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     if ((e = hipMalloc((void **)&c->d_seg_cnt, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_seg_off, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMalloc((void **)&c->d_bmask, 2 * kMaskWords * sizeof(unsigned long long))) !=
-            hipSuccess ||
-        (e = hipMemset(c->d_bmask, 0, 2 * kMaskWords * sizeof(unsigned long long))) !=
-            hipSuccess ||
         (e = hipMalloc((void **)&c->d_scan_status, (size_t)c->nb * (kMaxChunks / kScanTile) *
                                                        sizeof(unsigned long long))) != hipSuccess ||
         (e = hipHostMalloc((void **)&c->d_scan_fault, sizeof(uint32_t),
@@ -2838,7 +2751,6 @@ void yrss_fini(yrss_ctx *c)
     free_burst(c);
     (void)hipFree(c->d_seg_cnt);
     (void)hipFree(c->d_seg_off);
-    (void)hipFree(c->d_bmask);
     (void)hipFree(c->d_scan_status);
     (void)hipFree(c->d_rank);
     (void)hipHostFree(c->d_scan_fault);
@@ -2988,14 +2900,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     P.filter = b->filter;
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
-    // single-list short path: the parse kernel ORs the buckets it saw into
-    // this batch's mask set, the scan clears the other set for the next batch
-    const bool masked = compact && !ranked && !c->no_mask;
-    unsigned long long *bm_cur = c->d_bmask + (c->mask_par & 1u) * kMaskWords;
-    unsigned long long *bm_next = c->d_bmask + ((c->mask_par + 1u) & 1u) * kMaskWords;
-    if (masked)
-        ++c->mask_par;
-    P.bmask = masked ? bm_cur : nullptr;
     {
         Timed t(c, YRSS_K_PARSE_HASH);
         hipExtLaunchKernelGGL(pick_parse(c, ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
@@ -3019,9 +2923,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         if ((++c->scan_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
             ++c->scan_epoch;
         SP.epoch = c->scan_epoch;
-        SP.bmask = masked ? bm_cur : nullptr;
-        SP.bmask_next = bm_next;
-        SP.n = n;
         hipExtLaunchKernelGGL(yrss_seg_scan, dim3(c->nb * SP.tiles), dim3(kScanBlock), 0, s,
                               t.a, t.b, 0, SP);
     }
@@ -3044,7 +2945,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.rank = c->d_rank;
     // few-bucket groups build their lists in LDS when a group fits the image
     S.img = (!ranked && lay.seg <= kImgPkts && !c->no_img) ? 1u : 0u;
-    S.bmask = masked ? bm_cur : nullptr;
     {
         Timed t(c, YRSS_K_SCATTER);
         if (ranked)
