@@ -510,6 +510,8 @@ def main(argv=None):
     elapsed = max_over_ranks(t1 - t0, world)
     k_ms, k_cnt = eng.timing_read(abi.K_PARSE_HASH)
     k_avg_s = max_over_ranks(k_ms / max(k_cnt, 1) / 1e3, world)
+    k_med_s = max_over_ranks(eng.timing_quantile(abi.K_PARSE_HASH) / 1e3, world) \
+        if k_cnt else 0.0
     eng.timing_enable(0)
     # the scan and scatter shares, from a separate pass after the timed one:
     # events on all three kernels widen the step by ~9 us, so the timed steps
@@ -606,6 +608,7 @@ def main(argv=None):
                 "traffic": traffic,
                 "kernel": "yrss_parse_hash", "bytes_per_pkt": bpp,
                 "kernel_avg_us": round(k_avg_s * 1e6, 2),
+                "kernel_median_us": round(k_med_s * 1e6, 2),
                 "step": step,
                 "probe": None if probe_s is None else {
                     "what": "ideal-traffic twin (tools/yrss_probe.hip): same bytes, no parse",

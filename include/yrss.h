@@ -412,6 +412,9 @@ int yrss_synth_dev(yrss_ctx *ctx, const struct yrss_synth_params *p,
 int yrss_timing_enable(yrss_ctx *ctx, int kernel_mask);
 int yrss_timing_read(yrss_ctx *ctx, int kernel, double *total_ms,
                      uint32_t *launches);
+/* The q-quantile (0.5: median) of kernel k's per-launch
+ * durations since yrss_timing_enable, in ms; -ENODATA before any launch. */
+int yrss_timing_quantile(yrss_ctx *ctx, int kernel, double q, double *ms);
 
 /* ---- persistent burst worker ------------------------------------------------------ */
 

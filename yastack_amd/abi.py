@@ -146,6 +146,8 @@ _PROTOS = {
     "yrss_timing_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "yrss_timing_read": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(_u32)]),
+    "yrss_timing_quantile": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double,
+                                            ctypes.POINTER(ctypes.c_double)]),
     "yrss_grid_for": (_u32, [_vp, _u32]),
     "yrss_status": (ctypes.c_int, [_vp]),
     "yrss_wait": (ctypes.c_int, [_vp]),

@@ -2053,6 +2053,7 @@ struct yrss_ctx {
     std::vector<TimedPair> ev_pending;
     double ms[YRSS_K_COUNT] = {0, 0, 0};
     uint32_t launches[YRSS_K_COUNT] = {0, 0, 0};
+    std::vector<float> durs[YRSS_K_COUNT];   // per-launch ms since yrss_timing_enable
 };
 
 namespace {
@@ -3857,6 +3858,7 @@ int yrss_timing_enable(yrss_ctx *c, int enable)
     for (int k = 0; k < YRSS_K_COUNT; ++k) {
         c->ms[k] = 0.0;
         c->launches[k] = 0;
+        c->durs[k].clear();
     }
     return 0;
 }
@@ -3871,6 +3873,7 @@ int yrss_timing_read(yrss_ctx *c, int kernel, double *total_ms, uint32_t *launch
         YRSS_HIP(hipEventElapsedTime(&ms, p.a, p.b));
         c->ms[p.kernel] += ms;
         c->launches[p.kernel] += 1;
+        c->durs[p.kernel].push_back(ms);
         c->ev_free.push_back(p.a);
         c->ev_free.push_back(p.b);
     }
@@ -3879,6 +3882,22 @@ int yrss_timing_read(yrss_ctx *c, int kernel, double *total_ms, uint32_t *launch
         *total_ms = c->ms[kernel];
     if (launches)
         *launches = c->launches[kernel];
+    return 0;
+}
+
+int yrss_timing_quantile(yrss_ctx *c, int kernel, double q, double *ms)
+{
+    if (!c || kernel < 0 || kernel >= YRSS_K_COUNT || !ms || !(q >= 0.0 && q <= 1.0))
+        return -EINVAL;
+    int rc = yrss_timing_read(c, kernel, nullptr, nullptr);
+    if (rc)
+        return rc;
+    std::vector<float> d = c->durs[kernel];
+    if (d.empty())
+        return -ENODATA;
+    const size_t i = (size_t)(q * (double)(d.size() - 1) + 0.5);
+    std::nth_element(d.begin(), d.begin() + (ptrdiff_t)i, d.end());
+    *ms = d[i];
     return 0;
 }
 

@@ -402,6 +402,13 @@ class SoftRss:
                                              ctypes.byref(cnt)), "yrss_timing_read")
         return ms.value, cnt.value
 
+    def timing_quantile(self, kernel: int, q: float = 0.5) -> float:
+        """q-quantile of kernel's per-launch durations (ms) since timing_enable."""
+        ms = ctypes.c_double()
+        abi.check(self._lib.yrss_timing_quantile(self._ctx, kernel, q, ctypes.byref(ms)),
+                  "yrss_timing_quantile")
+        return ms.value
+
     def status(self) -> int:
         """Synchronise and return (then clear) the device-side fault state:
         0, or -EIO if the scan's look-back did not resolve (yrss_status)."""
