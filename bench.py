@@ -257,12 +257,13 @@ def cpu_baseline(args, nb_queues):
     reference's single dispatching lcore, ff_dpdk_if.c:1653) and on every core
     this job may use (at most 16: one GPU's share of the box), as independent
     processes pinned one per core.  `value` is the bit-serial port on 1 core
-    over the bench's own stream."""
+    over the bench's own stream (measured first, then udp4 and tcp4)."""
     cpus = sorted(os.sched_getaffinity(0))
     cpus_all = cpus[: max(1, min(16, len(cpus)))]
-    secs = max(0.5, args.cpu_seconds / (2 * len(CPU_PROFILES) * len(CPU_VARIANTS)))
+    profs = list(dict.fromkeys([args.profile, *CPU_PROFILES]))   # the bench's own stream first
+    secs = max(0.5, args.cpu_seconds / (2 * len(profs) * len(CPU_VARIANTS)))
     by = {}
-    for prof in CPU_PROFILES:
+    for prof in profs:
         by[prof] = {}
         for var in CPU_VARIANTS:
             by[prof][var] = {"1": round(_cpu_run(prof, var, secs, cpus_all[:1]), 2),
@@ -275,7 +276,7 @@ def cpu_baseline(args, nb_queues):
                 break
     except OSError:
         pass
-    head = args.profile if args.profile in by else "udp4"
+    head = args.profile
     return {
         "value": by[head]["bit_serial"]["1"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
         "sample": f"2^20 packets of each stream re-run for ~{secs:.1f}s per cell, one "
@@ -402,16 +403,17 @@ def pcie_fanout(profile: str, world: int):
     return out or None
 
 
-def load_traffic(path: str, key: dict):
-    """Per-launch HBM bytes for the parse kernel from a committed PMC summary
-    of the same workload (profiles/pmc_parse_hash.json), else None."""
+def load_traffic(path: str, key: dict, field: str = "hbm_bytes_per_launch"):
+    """Per-launch HBM bytes (parse kernel, or `step_hbm_bytes` for the whole
+    step) from a committed PMC summary of the same workload
+    (profiles/pmc_parse_hash.json), else None."""
     try:
         d = json.loads(Path(path).read_text())
     except (OSError, ValueError):
         return None
     for ent in d.get("entries", []):
         if all(ent.get("key", {}).get(k) == v for k, v in key.items()):
-            return ent.get("hbm_bytes_per_launch")
+            return ent.get(field)
     return None
 
 
@@ -545,6 +547,7 @@ def main(argv=None):
     key = {"profile": args.profile, "pkts": n, "stride": args.stride,
            "compact": not args.no_compact}
     traffic = load_traffic(args.pmc, key)
+    step["traffic"] = load_traffic(args.pmc, key, "step_hbm_bytes")
 
     check = None
     if args.check:
