@@ -466,6 +466,13 @@ def main(argv=None):
     from yastack_amd import SoftRss, abi
     from yastack_amd.shard import shard_range
 
+    # a launcher that gives each rank only its own GPU (HIP_VISIBLE_DEVICES per
+    # rank) leaves that GPU at ordinal 0; device_count() does not open the device
+    nvis = torch.cuda.device_count()
+    if nvis == 0:
+        raise SystemExit("bench.py: no GPU visible")
+    if local >= nvis:
+        local = local % nvis
     torch.cuda.set_device(local)
     devices = check_devices(device_identity(local, False), world)
     nbq = args.nb_queues or args.nb_procs
