@@ -108,3 +108,34 @@ def test_ballot_scatter_without_ranks(dev, oracle_mod, cfg):
             check(eng, oracle_mod, cfg, abi.SYN_FUZZ, 500001, first=11)
     with SoftRss(*cfg, device=0, max_burst=0) as eng:
         check(eng, oracle_mod, cfg, abi.SYN_FUZZ, 500001, first=11)
+
+
+@pytest.mark.parametrize("profile", [abi.SYN_UDP4, abi.SYN_TCP4, abi.SYN_IMIX])
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_unaligned_list_outputs(oracle_mod, profile, shift):
+    """qidx (and q / hash) at 4-byte but not 16-byte alignment, n not a
+    multiple of 4: the list paths' unaligned heads and tails (one-list
+    grid-stride path on UDP, LDS-image path on TCP / IMIX)."""
+    n, stride = 300007, 64
+    with SoftRss(3, 3, 1, 1, device=0, max_burst=0) as eng:
+        win, lens = eng.synth(profile, n, 17, stride=stride)
+        dev = win.device
+        qi_buf = torch.full((n + 8,), -1, dtype=torch.int32, device=dev)
+        q_buf = torch.empty(n + 8, dtype=torch.int16, device=dev)
+        h_buf = torch.empty(n + 8, dtype=torch.int32, device=dev)
+        qs = torch.empty(3 + 2, dtype=torch.int32, device=dev)
+        from yastack_amd.dispatch import DispatchResult
+        out = DispatchResult(q_buf[2 * shift:2 * shift + n], h_buf[shift:shift + n],
+                             qi_buf[shift:shift + n], qs)
+        res = eng.dispatch_dev(win, lens, stride, n, out=out)
+        torch.cuda.synchronize()
+        w_h = win[: n * stride].cpu().numpy()
+        l_h = lens[:n].cpu().numpy().view(np.uint16)
+        q_ref, h_ref = oracle_mod.dispatch_windows(w_h, stride, l_h, oracle_mod.cfg(3, 3, 1, 1))
+        qi_ref, qs_ref = oracle_mod.process_burst(q_ref, 3)
+        assert np.array_equal(res.q.cpu().numpy(), q_ref)
+        assert np.array_equal(res.hash.cpu().numpy().view(np.uint32), h_ref)
+        assert np.array_equal(qs.cpu().numpy().view(np.uint32), qs_ref)
+        qi_all = qi_buf.cpu().numpy()
+        assert np.array_equal(qi_all[shift:shift + n].view(np.uint32), qi_ref)
+        assert (qi_all[:shift] == -1).all() and (qi_all[shift + n:] == -1).all()   # no overrun
