@@ -59,7 +59,6 @@ constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this m
 constexpr uint32_t kRankStage = 1024;   // ranked scatter: chunk stage (packets) per wave
 constexpr uint32_t kImgPkts = 4096;     // few-bucket scatter: largest group built in LDS
 constexpr uint32_t kImgLine = 32;       // entries per 128-byte line
-constexpr uint32_t kImgWords = kImgPkts + 8u * 2u * kImgLine;   // + up to 2 lines of slack per bucket
 // Toeplitz key tables: the 96 tuple bits are cut into fields of kHashBits
 // (MSB first); table t maps a field value to the XOR of the key windows its
 // set bits select.  8: 12 byte tables of 256 words (12 lookups; random indices
@@ -125,7 +124,7 @@ struct ScatterParams {
     uint32_t gshift;           // a group is 2^gshift chunks
     uint32_t chunk;            // packets per chunk
     const uint16_t *rank;      // ranked mode: rank in chunk per packet (parse kCount == 2)
-    uint32_t img;              // few-bucket groups assemble their lists in LDS (seg <= kImgPkts)
+    uint32_t img;              // words of a wave's LDS list image (0: per-lane stores)
     uint32_t single;           // a batch feeding one list takes the grid-stride identity path
 };
 
@@ -1063,7 +1062,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     if (kseg <= kFewBuckets)
         scatter_few(P, off, gcnt, beg, end, lane,
                     P.img ? reinterpret_cast<uint32_t *>(smem) + kScatterWaves * 2u * P.nb +
-                                wave * kImgWords
+                                wave * P.img
                           : nullptr);
     else
         scatter_general(P, off, beg, end, lane);
@@ -2115,7 +2114,11 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     while ((1ull << ct_shift) < ct)
         ++ct_shift;
     ct = 1ull << ct_shift;
-    const uint64_t gt = c->group_tiles ? c->group_tiles : 64u;
+    // scatter groups: 2048 packets when every group takes the few-bucket LDS
+    // image path (nb <= 8: a 9-10 KB image per wave, 3-4 workgroups per CU;
+    // 4096 had half the occupancy, 1024 left more partial list lines dirty:
+    // profiles/r02_v10_group_ab.log), else 4096 (r01_v5_scatter_sweep.log)
+    const uint64_t gt = c->group_tiles ? c->group_tiles : (c->nb <= kFewBuckets ? 32u : 64u);
     Layout L;
     L.ct_shift = ct_shift;
     L.shift = 0;
@@ -2970,8 +2973,11 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.gshift = lay.shift;
     S.chunk = lay.chunk;
     S.rank = c->d_rank;
-    // few-bucket groups build their lists in LDS when a group fits the image
-    S.img = (!ranked && lay.seg <= kImgPkts && !c->no_img) ? 1u : 0u;
+    // few-bucket groups build their lists in LDS when a group fits the image:
+    // the group's packets plus up to two lines of slack per bucket
+    S.img = (!ranked && lay.seg <= kImgPkts && !c->no_img)
+                ? lay.seg + 2u * kImgLine * std::min<uint32_t>(c->nb, kFewBuckets)
+                : 0u;
     S.single = c->no_single ? 0u : 1u;
     {
         Timed t(c, YRSS_K_SCATTER);
@@ -2984,7 +2990,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         else
             hipExtLaunchKernelGGL(yrss_scatter, dim3(lay.nseg / kScatterWaves),
                                   dim3(kScatterBlock),
-                                  (uint32_t)(kScatterWaves * (2u * c->nb + (S.img ? kImgWords : 0u)) *
+                                  (uint32_t)(kScatterWaves * (2u * c->nb + S.img) *
                                              sizeof(uint32_t)),
                                   s, t.a, t.b, 0, S);
     }
