@@ -59,6 +59,7 @@ constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this m
 constexpr uint32_t kRankStage = 1024;   // ranked scatter: chunk stage (packets) per wave
 constexpr uint32_t kImgPkts = 4096;     // few-bucket scatter: largest group built in LDS
 constexpr uint32_t kImgLine = 32;       // entries per 128-byte line
+constexpr uint32_t kCntStride = 65;     // count mode: words per bucket's lane counters
 // Toeplitz key tables: the 96 tuple bits are cut into fields of kHashBits
 // (MSB first); table t maps a field value to the XOR of the key windows its
 // set bits select.  8: 12 byte tables of 256 words (12 lookups; random indices
@@ -126,6 +127,10 @@ struct ScatterParams {
     const uint16_t *rank;      // ranked mode: rank in chunk per packet (parse kCount == 2)
     uint32_t img;              // words of a wave's LDS list image (0: per-lane stores)
     uint32_t single;           // a batch feeding one list takes the grid-stride identity path
+    uint32_t aux;              // words of a wave's LDS cursors ahead of its image
+    uint32_t wlds;             // words of LDS per wave
+    uint32_t cnt_off;          // count mode: wave LDS word offset of its counters (0: off)
+    uint32_t kmin;             // count mode for groups feeding more than kmin buckets
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -924,7 +929,178 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const u
     }
 }
 
-// General case, any number of buckets, cost independent of nb.  off[b] in LDS
+// Image layout of a group's runs (count mode): bucket b's run [off[b],
+// off[b] + gcnt[b]) is placed at image lines of its own, aligned as its global
+// lines are, so image word w of those lines is global slot w - io (io = the
+// run's image line start minus its global line start).  icur[b] is the run's
+// first image slot; desc[L] = {io, a, e, 0} describes image line L by its
+// run [a, e).  Returns the image words used (a multiple of kImgLine; at most
+// the group's packets + 62 per bucket).
+__device__ __forceinline__ uint32_t image_layout(uint32_t nb, const uint32_t *off,
+                                                 const uint32_t *gcnt, uint32_t *icur,
+                                                 u32x4 *desc, uint32_t lane)
+{
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += kWave) {
+        const uint32_t b = b0 + lane;
+        const uint32_t cnt = b < nb ? gcnt[b] : 0u, a = b < nb ? off[b] : 0u;
+        const uint32_t span =
+            cnt ? (((a & (kImgLine - 1u)) + cnt + kImgLine - 1u) & ~(kImgLine - 1u)) : 0u;
+        const uint32_t x = wave_incl_scan(span, lane);
+        const uint32_t ib = carry + x - span;
+        if (b < nb)
+            icur[b] = ib + (a & (kImgLine - 1u));
+        const u32x4 d = {ib - (a & ~(kImgLine - 1u)), a, a + cnt, 0u};
+        for (uint32_t L = ib / kImgLine; L < (ib + span) / kImgLine; ++L)
+            desc[L] = d;
+        carry += __shfl(x, kWave - 1, kWave);
+    }
+    return carry;
+}
+
+// Writes a group's image (image_layout) out: each lane takes 16 bytes of an
+// image line.  Lines wholly inside their run leave as 16-byte non-temporal
+// stores; the partial lines at a run's ends are shared with the neighbouring
+// groups' runs and go out as plain 4-byte stores, merged in L2.
+__device__ __forceinline__ void flush_image(const ScatterParams &P, const uint32_t *img,
+                                            const u32x4 *desc, uint32_t words, uint32_t lane)
+{
+#pragma unroll 2
+    for (uint32_t v = lane; v < words / 4u; v += kWave) {
+        const uint32_t w = 4u * v;
+        const u32x4 d = desc[w / kImgLine];
+        const u32x4 x = *reinterpret_cast<const u32x4 *>(img + w);
+        const uint32_t g = w - d[0], gl = g & ~(kImgLine - 1u);
+        if (gl >= d[1] && gl + kImgLine <= d[2]) {
+            __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(P.qidx + g));
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; ++k)
+                if (g + k >= d[1] && g + k < d[2])
+                    P.qidx[g + k] = x[k];
+        }
+    }
+}
+
+// Count mode: the group's q, lane-major (lane l holds packets l*M .. l*M + M-1,
+// M = seg / 64), loaded straight into registers as 16-byte loads first thing
+// in the kernel, so they are in flight while the group's layout is worked
+// out.  Past the batch's end the slots are left 0 (the tail group never reads
+// them, kFull false).
+template <int M>
+__device__ __forceinline__ void count_load(const ScatterParams &P, uint32_t beg, uint32_t end,
+                                           uint32_t lane, u32x4 (&raw)[M / 8])
+{
+    const uint32_t p = beg + lane * (uint32_t)M;
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(P.q + p);
+#pragma unroll
+    for (int i = 0; i < M / 8; ++i) {
+        if (p + 8u * i + 8u <= end) {
+            raw[i] = __builtin_nontemporal_load(src + i);
+        } else {
+            uint32_t h[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8u; ++k)
+                h[k] = p + 8u * i + k < end ? (uint16_t)P.q[p + 8u * i + k] : 0u;
+            raw[i] = u32x4{h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16,
+                           h[6] | h[7] << 16};
+        }
+    }
+}
+
+// Count mode for groups feeding many buckets: a lane-serial counting sort.
+// A packet's stable rank in its bucket is the bucket's count in lower lanes
+// plus its count among the lane's earlier packets, so there are no ballots,
+// no branches and no counters shared between lanes, and the cost per packet
+// does not depend on the bucket count (the few-bucket path's ranking costs ~5
+// VALU per packet and bucket).  A bucket is min(q as u16, nq) (a negative q is
+// >= 0x8000 as u16, so it lands in the drop bucket nq, as bucket_of), counter
+// cnt[b * 65 + l] is lane l's for bucket b: conflict-free, ~2 VALU per packet
+// to count and ~4 to place.  After the scan over lanes each counter is the
+// lane's next image slot in its bucket.  kFull: the group is whole (else
+// slots past the batch's end are skipped).
+template <int M, bool kFull>
+__device__ __forceinline__ void count_pass(const ScatterParams &P, const u32x4 (&raw)[M / 8],
+                                           uint32_t *mine, uint32_t *img, uint32_t p0,
+                                           uint32_t len, bool place)
+{
+    // 16 packets a batch: their counter bumps go out back to back and the
+    // image stores follow (counters and image are disjoint), so a batch
+    // waits for LDS once rather than once per packet
+    constexpr int kB = 16;
+#pragma unroll
+    for (int e0 = 0; e0 < M; e0 += kB) {
+        uint32_t slot[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+            const uint32_t e = e0 + k;
+            const uint32_t x = raw[e / 8][(e / 2) & 3];
+            const uint32_t b = min((e & 1) ? (x >> 16) : (x & 0xffffu), P.nq);
+            uint32_t *c = mine + b * kCntStride;
+            slot[k] = 0;
+            if (kFull || e < len) {
+                if (place)
+                    slot[k] = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WAVEFRONT);
+                else
+                    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+        }
+        if (place) {
+#pragma unroll
+            for (int k = 0; k < kB; ++k)
+                if (kFull || (uint32_t)(e0 + k) < len)
+                    img[slot[k]] = p0 + (uint32_t)(e0 + k);
+        }
+    }
+}
+
+template <int M>
+__device__ __forceinline__ void scatter_count(const ScatterParams &P, const u32x4 (&raw)[M / 8],
+                                              const uint32_t *icur, uint32_t *img,
+                                              uint32_t *cnt, uint32_t beg, uint32_t end,
+                                              uint32_t lane)
+{
+    for (uint32_t i = lane; i < P.nb * kCntStride; i += kWave)
+        cnt[i] = 0;
+    wave_lds_sync();
+    uint32_t *mine = cnt + lane;
+    const uint32_t p0 = beg + lane * (uint32_t)M;
+    const uint32_t len = p0 < end ? end - p0 : 0u;   // the lane's packets (M if whole)
+    const bool full = end - beg == (uint32_t)(M * kWave);
+    if (full)
+        count_pass<M, true>(P, raw, mine, img, p0, len, false);
+    else
+        count_pass<M, false>(P, raw, mine, img, p0, len, false);
+    wave_lds_sync();
+    // exclusive scan over lanes, transposed: lane b walks bucket b's 64
+    // counters (stride kCntStride keeps both access patterns conflict-free)
+    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+        const uint32_t b = b0 + lane;
+        if (b < P.nb) {
+            uint32_t run = icur[b];
+            uint32_t *row = cnt + b * kCntStride;
+            for (uint32_t l = 0; l < (uint32_t)kWave; l += 8u) {
+                uint32_t x[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    x[k] = row[l + k];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    row[l + k] = run;
+                    run += x[k];
+                }
+            }
+        }
+    }
+    wave_lds_sync();
+    if (full)
+        count_pass<M, true>(P, raw, mine, img, p0, len, true);
+    else
+        count_pass<M, false>(P, raw, mine, img, p0, len, true);
+}
+
+// General case, any number of buckets, cost independent of nb.  cur[b] in LDS
 // is bucket b's output cursor for this segment.  Per slot, peers (lanes sharing
 // a bucket) come from bit-sliced ballots; the group's lowest lane bumps the
 // cursor with an LDS atomic whose return value is the group's first output
@@ -933,7 +1109,7 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const u
 // leader's value by ds_bpermute and add their rank inside the group.  Stores
 // go straight from registers.  A full round that is all one bucket (UDP
 // stretches) skips the ballots.
-__device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t beg,
+__device__ void scatter_general(const ScatterParams &P, uint32_t *cur, uint32_t beg,
                                 uint32_t end, uint32_t lane)
 {
     constexpr uint32_t kRound = kWave * kScatterRound;
@@ -957,13 +1133,13 @@ __device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t 
         for (int j = 0; j < kScatterRound; ++j)
             same &= bk[j] == B0;
         if (end - r0 >= kRound && __all(same)) {
-            const uint32_t base = __builtin_amdgcn_readfirstlane(off[B0]);
+            const uint32_t base = __builtin_amdgcn_readfirstlane(cur[B0]);
 #pragma unroll
             for (int j = 0; j < kScatterRound; ++j)
                 P.qidx[base + j * kWave + lane] = r0 + j * kWave + lane;
             wave_lds_sync();
             if (lane == 0)
-                off[B0] = base + kRound;
+                cur[B0] = base + kRound;
             wave_lds_sync();
             continue;
         }
@@ -976,7 +1152,7 @@ __device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t 
         for (int j = 0; j < kScatterRound; ++j) {
             first[j] = 0;
             if (((vmask >> j) & 1u) && (peers[j] & lt) == 0)
-                first[j] = atomicAdd(&off[bk[j]], (uint32_t)__popcll(peers[j]));
+                first[j] = atomicAdd(&cur[bk[j]], (uint32_t)__popcll(peers[j]));
         }
 #pragma unroll
         for (int j = 0; j < kScatterRound; ++j) {
@@ -992,42 +1168,76 @@ __device__ void scatter_general(const ScatterParams &P, uint32_t *off, uint32_t 
 
 // ---------------------------------------------------------------------------
 // Kernel 3: stable scatter of packet indices into per-bucket lists.
+// Persistent: as many waves as are resident, wave w taking groups w, w + W,
+// ... (W waves; the waves in flight together cover one stretch of the batch,
+// as a wave per group did).  A wave works out the lists' starts once, and while it works on a
+// group the next group's bucket prefixes (and, in count mode, its q) are
+// already in flight: one wave per group paid those loads' latency once per
+// group (13 us of a 22 us all-TCP scatter at 2^24 packets, 25 us with 65
+// buckets, where LDS left two waves per CU).
+// M > 0: groups of 64 * M packets feeding more than P.kmin buckets take
+// count mode.
 // ---------------------------------------------------------------------------
+constexpr uint32_t kBktChunks = (YRSS_MAX_QUEUES + 1 + kWave - 1) / kWave;
+
+template <int M>
 __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t lane = lane_id();
-    // per wave: off[nb], the group's output cursor per bucket; gcnt[nb], the
-    // group's packet count per bucket
-    uint32_t *off = reinterpret_cast<uint32_t *>(smem) + wave * 2u * P.nb;
+    // per wave: start[nb], the lists' starts; off[nb], the group's output
+    // cursor per bucket; gcnt[nb], the group's packet count per bucket;
+    // icur[nb], the image cursors (count mode); the list image; in count mode
+    // the image's line descriptors and the lanes' counters
+    uint32_t *start = reinterpret_cast<uint32_t *>(smem) + wave * P.wlds;
+    uint32_t *off = start + P.nb;
     uint32_t *gcnt = off + P.nb;
-    const uint32_t gw = blockIdx.x * kScatterWaves + wave;
+    uint32_t *icur = gcnt + P.nb;
+    uint32_t *img = start + P.aux;
+    const uint32_t W = gridDim.x * (blockDim.x / kWave);
+    const uint32_t gw = blockIdx.x * (blockDim.x / kWave) + wave;
+    const uint32_t ng = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
+    auto bounds = [&](uint32_t g, uint32_t &beg, uint32_t &end) {
+        beg = g * P.seg;
+        end = P.n - beg > P.seg ? beg + P.seg : P.n;
+    };
+    // a bucket's prefix at chunk column c (the total past the last chunk)
+    auto prefix = [&](uint32_t b, uint32_t c, uint32_t t) {
+        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : t;
+    };
 
-    // start[b] = exclusive scan of totals; off[b] = start[b] + the prefix at
-    // the group's first chunk; kseg = buckets this group feeds
-    const uint32_t col = gw << P.gshift, col_end = col + (1u << P.gshift);
-    uint32_t carry = 0, kseg = 0, nzb = 0;
-    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-        const uint32_t b = b0 + lane;
+    u32x4 raw[M > 0 ? M / 8 : 1];
+    if constexpr (M > 0) {
+        if (gw < ng) {
+            uint32_t beg, end;
+            bounds(gw, beg, end);
+            count_load<M>(P, beg, end, lane, raw);
+        }
+    }
+    // list starts (exclusive scan of totals); the first group's prefixes
+    // (o: at its first chunk, oe: at the next group's)
+    uint32_t carry = 0, nzb = 0;
+    uint32_t tot[kBktChunks], oe[kBktChunks];
+    const uint32_t col0 = gw << P.gshift, col1 = col0 + (1u << P.gshift);
+#pragma unroll
+    for (uint32_t i = 0; i < kBktChunks; ++i) {
+        tot[i] = oe[i] = 0;
+        if (i * kWave >= P.nb)
+            continue;
+        const uint32_t b = i * kWave + lane;
         const uint32_t t = b < P.nb ? P.totals[b] : 0u;
+        tot[i] = t;
         nzb += (uint32_t)__popcll(__ballot(t != 0u));
         const uint32_t x = wave_incl_scan(t, lane);
-        const uint32_t start = carry + x - t;
-        uint32_t o = t, oe = t;
         if (b < P.nb) {
-            const uint32_t *row = P.seg_off + (size_t)b * P.ncol;
-            if (col < P.nchunk)
-                o = row[col];
-            if (col_end < P.nchunk)
-                oe = row[col_end];
-        }
-        kseg += (uint32_t)__popcll(__ballot(b < P.nb && oe != o));
-        if (b < P.nb) {
-            off[b] = start + o;
-            gcnt[b] = oe - o;
+            start[b] = carry + x - t;
             if (gw == 0)
-                P.qstart[b] = start;
+                P.qstart[b] = carry + x - t;
+            if (gw < ng) {
+                off[b] = prefix(b, col0, t);   // o, until the group's loop adds start
+                oe[i] = prefix(b, col1, t);
+            }
         }
         carry += __shfl(x, kWave - 1, kWave);
     }
@@ -1054,18 +1264,76 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
             P.qidx[t] = t;
         return;
     }
-    wave_lds_sync();
-
-    const uint64_t beg64 = (uint64_t)gw * P.seg;
-    const uint32_t beg = beg64 < P.n ? (uint32_t)beg64 : P.n;
-    const uint32_t end = (uint64_t)beg + P.seg < P.n ? beg + P.seg : P.n;
-    if (kseg <= kFewBuckets)
-        scatter_few(P, off, gcnt, beg, end, lane,
-                    P.img ? reinterpret_cast<uint32_t *>(smem) + kScatterWaves * 2u * P.nb +
-                                wave * P.img
-                          : nullptr);
-    else
-        scatter_general(P, off, beg, end, lane);
+    for (uint32_t g = gw; g < ng; g += W) {
+        uint32_t beg, end;
+        bounds(g, beg, end);
+        // this group's cursors and counts from the prefetched prefixes, then
+        // the next group's prefixes in flight
+        const bool more = g + W < ng;
+        uint32_t kseg = 0, on[kBktChunks], oen[kBktChunks];
+        const uint32_t cn = (g + W) << P.gshift, cne = cn + (1u << P.gshift);
+#pragma unroll
+        for (uint32_t i = 0; i < kBktChunks; ++i) {
+            on[i] = oen[i] = 0;
+            if (i * kWave >= P.nb)
+                continue;
+            const uint32_t b = i * kWave + lane;
+            uint32_t cnt = 0;
+            if (b < P.nb) {
+                const uint32_t o = off[b];
+                off[b] = start[b] + o;
+                cnt = oe[i] - o;
+                gcnt[b] = cnt;
+                if (more) {
+                    on[i] = prefix(b, cn, tot[i]);
+                    oen[i] = prefix(b, cne, tot[i]);
+                }
+            }
+            kseg += (uint32_t)__popcll(__ballot(cnt != 0u));
+        }
+        wave_lds_sync();
+        if constexpr (M > 0) {
+            if (kseg > P.kmin) {
+                // the host sized the image for the group + 62 words per bucket
+                u32x4 *desc = reinterpret_cast<u32x4 *>(img + P.img);
+                const uint32_t words = image_layout(P.nb, off, gcnt, icur, desc, lane);
+                wave_lds_sync();
+                scatter_count<M>(P, raw, icur, img, start + P.cnt_off, beg, end, lane);
+                if (more) {
+                    uint32_t nb0, ne0;
+                    bounds(g + W, nb0, ne0);
+                    count_load<M>(P, nb0, ne0, lane, raw);
+                }
+                wave_lds_sync();
+                flush_image(P, img, desc, words, lane);
+                goto next;
+            }
+            if (more) {
+                uint32_t nb0, ne0;
+                bounds(g + W, nb0, ne0);
+                count_load<M>(P, nb0, ne0, lane, raw);
+            }
+        }
+        if (kseg <= kFewBuckets)
+            scatter_few(P, off, gcnt, beg, end, lane, P.img ? img : nullptr);
+        else
+            scatter_general(P, off, beg, end, lane);
+    next:
+        // the next group's prefixes (off is free again once the wave's LDS
+        // work above is done)
+        wave_lds_sync();
+#pragma unroll
+        for (uint32_t i = 0; i < kBktChunks; ++i) {
+            if (i * kWave >= P.nb)
+                continue;
+            const uint32_t b = i * kWave + lane;
+            if (b < P.nb) {
+                off[b] = on[i];
+                oe[i] = oen[i];
+            }
+        }
+        wave_lds_sync();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1083,14 +1351,13 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterPara
     // per wave: start[nb] list starts; cur[nb] the chunk's global cursor per
     // bucket; lst[nb] the bucket's first slot in the chunk's sorted stage;
     // stage[chunk] packet index | bucket << ... (two arrays)
-    uint32_t *wbase = reinterpret_cast<uint32_t *>(smem) +
-                      wave * (3u * P.nb + 2u * kRankStage);
+    uint32_t *wbase = reinterpret_cast<uint32_t *>(smem) + wave * P.wlds;
     uint32_t *start = wbase;
     uint32_t *cur = start + P.nb;
     uint32_t *lst = cur + P.nb;
     uint32_t *sidx = lst + P.nb;
     uint32_t *sbk = sidx + kRankStage;
-    const uint32_t gw = blockIdx.x * kScatterWaves + wave;
+    const uint32_t gw = blockIdx.x * (blockDim.x / kWave) + wave;
 
     uint32_t carry = 0;
     for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
@@ -1957,6 +2224,16 @@ struct yrss_ctx {
     bool no_rank = false;           // YRSS_NO_RANK: ballot scatter even for many buckets
     bool no_img = false;            // YRSS_NO_IMG: few-bucket lists stored per lane, not via LDS
     bool no_single = false;         // YRSS_NO_SINGLE: no grid-stride path for one-list batches
+    bool no_count = false;          // YRSS_NO_COUNT: no count-mode scatter
+    bool scatter_full = false;      // YRSS_SCATTER_FULL: a scatter wave per group
+    struct Occ {
+        const void *fn;
+        uint32_t block, lds, blocks;
+    };
+    std::vector<Occ> occ;           // resident_blocks cache
+    uint32_t count_kmin = kFewBuckets;   // YRSS_COUNT_KMIN: count mode above this many buckets
+    uint32_t count_max_nb = 17;     // YRSS_COUNT_MAXNB: count mode up to this many buckets
+    uint32_t scatter_wpb = 0;       // YRSS_SCATTER_WPB: waves per scatter workgroup (0: auto)
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
     uint32_t *d_scan_fault = nullptr;   // host-coherent pinned word (yrss_status)
@@ -2114,11 +2391,14 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     while ((1ull << ct_shift) < ct)
         ++ct_shift;
     ct = 1ull << ct_shift;
-    // scatter groups: 2048 packets when every group takes the few-bucket LDS
-    // image path (nb <= 8: a 9-10 KB image per wave, 3-4 workgroups per CU;
-    // 4096 had half the occupancy, 1024 left more partial list lines dirty:
-    // profiles/r02_v10_group_ab.log), else 4096 (r01_v5_scatter_sweep.log)
-    const uint64_t gt = c->group_tiles ? c->group_tiles : (c->nb <= kFewBuckets ? 32u : 64u);
+    // scatter groups: 2048 packets for the few-bucket LDS image path (nb <=
+    // 8: a 9-10 KB image per wave, 3-4 workgroups per CU; 4096 had half the
+    // occupancy, 1024 left more partial list lines dirty:
+    // profiles/r02_v10_group_ab.log), count mode (10..17 buckets) and the
+    // ballot path past 65 buckets; 4096 for the ranked path (18..65 buckets,
+    // r01_v5_scatter_sweep.log, profiles/r02_v11_count_sweep.log)
+    const uint64_t gt = c->group_tiles ? c->group_tiles
+                                       : (c->nb <= 17u || c->nb > 65u ? 32u : 64u);
     Layout L;
     L.ct_shift = ct_shift;
     L.shift = 0;
@@ -2132,6 +2412,82 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     L.nseg = (uint32_t)((((uint64_t)n + L.seg - 1) / L.seg + kScatterWaves - 1) /
                         kScatterWaves * kScatterWaves);
     return L;
+}
+
+// LDS of one scatter wave: its cursors (aux words), the group's list image
+// (img words, 0 = none) and, in count mode (cnt_off != 0), the image's line
+// descriptors and the lanes' counters; wpb waves per workgroup, halved until
+// a workgroup holds at most 64 KiB.  m: count mode's packets per lane (0 =
+// off).  A few-bucket image holds the group plus two lines per bucket up to
+// kFewBuckets; a count-mode one two lines for every bucket, image_layout's
+// bound.
+struct ScatterLds {
+    uint32_t aux, img, wlds, wpb, cnt_off, m;
+};
+constexpr uint32_t kScatterLdsMax = 64u * 1024u / 4u;   // words per workgroup
+
+void scatter_wpb(const yrss_ctx *c, ScatterLds &r)
+{
+    r.wpb = c->scatter_wpb ? c->scatter_wpb : (uint32_t)kScatterWaves;
+    while (r.wpb > 1 && r.wpb * r.wlds > kScatterLdsMax)
+        r.wpb /= 2;
+}
+
+// Count mode: for 10..count_max_nb (17) buckets by default.  With 9 the
+// groups rarely feed more than 8 (nb_procs 8 with dispatch_only_core hashes
+// to 7 queues), and count mode's larger LDS share and unused q loads cost the
+// few-bucket path 8 %; past 17 buckets the ranked path is as fast or faster
+// (runs of a line or two leave the image's whole-line stores little to do:
+// profiles/r02_v11_count_sweep.log).  It needs 32 or 64 packets per lane and
+// its image and counters within one wave's LDS share.
+ScatterLds count_lds(const yrss_ctx *c, const Layout &lay)
+{
+    ScatterLds r{};
+    const uint32_t nb = c->nb;
+    if (c->no_img || c->no_count || nb <= c->count_kmin + 1u || nb > c->count_max_nb ||
+        (lay.seg != 2048u && lay.seg != 4096u))
+        return r;
+    r.m = lay.seg / kWave;
+    r.aux = (4u * nb + 3u) & ~3u;
+    r.img = lay.seg + 2u * kImgLine * nb;
+    r.cnt_off = r.aux + r.img + r.img / kImgLine * 4u;
+    r.wlds = (r.cnt_off + kCntStride * nb + 3u) & ~3u;
+    if (r.wlds > kScatterLdsMax)
+        return ScatterLds{};
+    scatter_wpb(c, r);
+    return r;
+}
+
+ScatterLds scatter_lds(const yrss_ctx *c, const Layout &lay, bool ranked)
+{
+    const uint32_t nb = c->nb;
+    ScatterLds r{};
+    if (ranked) {
+        r.wlds = 3u * nb + 2u * kRankStage;
+    } else {
+        r.aux = (4u * nb + 3u) & ~3u;
+        if (!c->no_img && lay.seg <= kImgPkts)
+            r.img = lay.seg + 2u * kImgLine * std::min(nb, kFewBuckets);
+        r.wlds = r.aux + r.img;
+    }
+    scatter_wpb(c, r);
+    return r;
+}
+
+// Workgroups of kernel fn (block threads, lds bytes) resident on the whole
+// device at once, from the occupancy calculator, cached per context.
+uint32_t resident_blocks(yrss_ctx *c, const void *fn, uint32_t block, uint32_t lds)
+{
+    for (const auto &e : c->occ)
+        if (e.fn == fn && e.block == block && e.lds == lds)
+            return e.blocks;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)block, lds) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    const uint32_t blocks = (uint32_t)per_cu * (uint32_t)c->cus;
+    c->occ.push_back({fn, block, lds, blocks});
+    return blocks;
 }
 
 typedef void (*ParseKernel)(ParseParams);
@@ -2675,6 +3031,25 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         c->no_img = atoi(e) != 0;
     if (const char *e = getenv("YRSS_NO_SINGLE"))
         c->no_single = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_NO_COUNT"))
+        c->no_count = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_COUNT_MAXNB")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= YRSS_MAX_QUEUES + 1)
+            c->count_max_nb = (uint32_t)v;
+    }
+    if (const char *e = getenv("YRSS_SCATTER_FULL"))
+        c->scatter_full = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_COUNT_KMIN")) {
+        const int v = atoi(e);
+        if (v >= 1 && v <= 256)
+            c->count_kmin = (uint32_t)v;
+    }
+    if (const char *e = getenv("YRSS_SCATTER_WPB")) {
+        const int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4)
+            c->scatter_wpb = (uint32_t)v;
+    }
     if (const char *e = getenv("YRSS_GROUP_TILES")) {
         const int v = atoi(e);
         if (v >= 1 && v <= 65536)
@@ -2900,7 +3275,9 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     // buckets, -2 % at 17; at 10 buckets (256-packet chunks) the ranks' cost in
     // the parse kernel (+5-8 us) outweighed the gain, and chunks above
     // kRankStage packets do not fit the stage.
-    const bool ranked = compact && !c->no_rank && c->nb > 17u && lay.chunk <= kRankStage;
+    const ScatterLds cl = compact ? count_lds(c, lay) : ScatterLds{};
+    const bool ranked =
+        compact && !c->no_rank && !cl.cnt_off && c->nb > 17u && lay.chunk <= kRankStage;
     if (ranked && c->rank_cap < n) {
         if (c->d_rank) {
             YRSS_HIP(hipStreamSynchronize(s));
@@ -2973,26 +3350,24 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.gshift = lay.shift;
     S.chunk = lay.chunk;
     S.rank = c->d_rank;
-    // few-bucket groups build their lists in LDS when a group fits the image:
-    // the group's packets plus up to two lines of slack per bucket
-    S.img = (!ranked && lay.seg <= kImgPkts && !c->no_img)
-                ? lay.seg + 2u * kImgLine * std::min<uint32_t>(c->nb, kFewBuckets)
-                : 0u;
     S.single = c->no_single ? 0u : 1u;
+    const ScatterLds sl = cl.cnt_off ? cl : scatter_lds(c, lay, ranked);
+    S.aux = sl.aux;
+    S.img = sl.img;
+    S.wlds = sl.wlds;
+    S.cnt_off = sl.cnt_off;
+    S.kmin = c->count_kmin;
     {
+        void (*fn)(ScatterParams) = ranked          ? yrss_scatter_ranked
+                                    : sl.m == 64u ? yrss_scatter<64>
+                                    : sl.m == 32u ? yrss_scatter<32>
+                                                  : yrss_scatter<0>;
+        const uint32_t lds = (uint32_t)(sl.wpb * sl.wlds * sizeof(uint32_t));
+        uint32_t grid = lay.nseg / sl.wpb;
+        if (!ranked && !c->scatter_full)   // persistent: the resident workgroups only
+            grid = std::min(grid, resident_blocks(c, (const void *)fn, sl.wpb * kWave, lds));
         Timed t(c, YRSS_K_SCATTER);
-        if (ranked)
-            hipExtLaunchKernelGGL(yrss_scatter_ranked, dim3(lay.nseg / kScatterWaves),
-                                  dim3(kScatterBlock),
-                                  (uint32_t)(kScatterWaves * (3u * c->nb + 2u * kRankStage) *
-                                             sizeof(uint32_t)),
-                                  s, t.a, t.b, 0, S);
-        else
-            hipExtLaunchKernelGGL(yrss_scatter, dim3(lay.nseg / kScatterWaves),
-                                  dim3(kScatterBlock),
-                                  (uint32_t)(kScatterWaves * (2u * c->nb + S.img) *
-                                             sizeof(uint32_t)),
-                                  s, t.a, t.b, 0, S);
+        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(sl.wpb * kWave), lds, s, t.a, t.b, 0, S);
     }
     YRSS_HIP(hipGetLastError());
     return 0;
