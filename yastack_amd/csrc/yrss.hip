@@ -1178,8 +1178,6 @@ __device__ void scatter_general(const ScatterParams &P, uint32_t *cur, uint32_t 
 // M > 0: groups of 64 * M packets feeding more than P.kmin buckets take
 // count mode.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kBktChunks = (YRSS_MAX_QUEUES + 1 + kWave - 1) / kWave;
-
 template <int M>
 __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
 {
@@ -1202,9 +1200,9 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
         beg = g * P.seg;
         end = P.n - beg > P.seg ? beg + P.seg : P.n;
     };
-    // a bucket's prefix at chunk column c (the total past the last chunk)
-    auto prefix = [&](uint32_t b, uint32_t c, uint32_t t) {
-        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : t;
+    // a bucket's prefix at chunk column c (its total past the last chunk)
+    auto prefix = [&](uint32_t b, uint32_t c) {
+        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : P.totals[b];
     };
 
     u32x4 raw[M > 0 ? M / 8 : 1];
@@ -1215,34 +1213,29 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
             count_load<M>(P, beg, end, lane, raw);
         }
     }
-    // list starts (exclusive scan of totals); the first group's prefixes
-    // (o: at its first chunk, oe: at the next group's)
+    // list starts (exclusive scan of totals)
     uint32_t carry = 0, nzb = 0;
-    uint32_t tot[kBktChunks], oe[kBktChunks];
-    const uint32_t col0 = gw << P.gshift, col1 = col0 + (1u << P.gshift);
-#pragma unroll
-    for (uint32_t i = 0; i < kBktChunks; ++i) {
-        tot[i] = oe[i] = 0;
-        if (i * kWave >= P.nb)
-            continue;
-        const uint32_t b = i * kWave + lane;
+    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+        const uint32_t b = b0 + lane;
         const uint32_t t = b < P.nb ? P.totals[b] : 0u;
-        tot[i] = t;
         nzb += (uint32_t)__popcll(__ballot(t != 0u));
         const uint32_t x = wave_incl_scan(t, lane);
         if (b < P.nb) {
             start[b] = carry + x - t;
             if (gw == 0)
                 P.qstart[b] = carry + x - t;
-            if (gw < ng) {
-                off[b] = prefix(b, col0, t);   // o, until the group's loop adds start
-                oe[i] = prefix(b, col1, t);
-            }
         }
         carry += __shfl(x, kWave - 1, kWave);
     }
     if (gw == 0 && lane == 0)
         P.qstart[P.nb] = carry;
+    // buckets 0..63's prefixes for the wave's first group (o: at its first
+    // chunk, oe: at the next group's); more buckets load theirs per group
+    uint32_t o0 = 0, oe0 = 0;
+    if (gw < ng && lane < P.nb) {
+        o0 = prefix(lane, gw << P.gshift);
+        oe0 = prefix(lane, (gw + 1u) << P.gshift);
+    }
     if (nzb == 1 && P.single) {
         // the batch feeds one list (all-UDP traffic): it starts at 0 and is
         // 0, 1, ..., n-1.  Written grid-stride as 16-byte non-temporal stores,
@@ -1267,29 +1260,25 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     for (uint32_t g = gw; g < ng; g += W) {
         uint32_t beg, end;
         bounds(g, beg, end);
-        // this group's cursors and counts from the prefetched prefixes, then
-        // the next group's prefixes in flight
+        // this group's cursors and counts, then the next group's prefixes in
+        // flight
         const bool more = g + W < ng;
-        uint32_t kseg = 0, on[kBktChunks], oen[kBktChunks];
-        const uint32_t cn = (g + W) << P.gshift, cne = cn + (1u << P.gshift);
-#pragma unroll
-        for (uint32_t i = 0; i < kBktChunks; ++i) {
-            on[i] = oen[i] = 0;
-            if (i * kWave >= P.nb)
-                continue;
-            const uint32_t b = i * kWave + lane;
+        const uint32_t col = g << P.gshift, col_end = col + (1u << P.gshift);
+        uint32_t kseg = 0;
+        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+            const uint32_t b = b0 + lane;
             uint32_t cnt = 0;
             if (b < P.nb) {
-                const uint32_t o = off[b];
+                const uint32_t o = b0 ? prefix(b, col) : o0;
+                cnt = (b0 ? prefix(b, col_end) : oe0) - o;
                 off[b] = start[b] + o;
-                cnt = oe[i] - o;
                 gcnt[b] = cnt;
-                if (more) {
-                    on[i] = prefix(b, cn, tot[i]);
-                    oen[i] = prefix(b, cne, tot[i]);
-                }
             }
             kseg += (uint32_t)__popcll(__ballot(cnt != 0u));
+        }
+        if (more && lane < P.nb) {
+            o0 = prefix(lane, (g + W) << P.gshift);
+            oe0 = prefix(lane, (g + W + 1u) << P.gshift);
         }
         wave_lds_sync();
         if constexpr (M > 0) {
@@ -1319,19 +1308,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
         else
             scatter_general(P, off, beg, end, lane);
     next:
-        // the next group's prefixes (off is free again once the wave's LDS
-        // work above is done)
-        wave_lds_sync();
-#pragma unroll
-        for (uint32_t i = 0; i < kBktChunks; ++i) {
-            if (i * kWave >= P.nb)
-                continue;
-            const uint32_t b = i * kWave + lane;
-            if (b < P.nb) {
-                off[b] = on[i];
-                oe[i] = oen[i];
-            }
-        }
+        // the wave's LDS is reused by its next group
         wave_lds_sync();
     }
 }
