@@ -1,6 +1,6 @@
 """Count-mode scatter parity (GPU).
 
-With 10..17 buckets (by default; YRSS_COUNT_MAXNB raises the bound), groups
+With 10..25 buckets (by default; YRSS_COUNT_MAXNB moves the bound), groups
 that feed more than YRSS_COUNT_KMIN buckets (default 8) are ranked by a
 lane-serial counting sort in LDS and leave through the LDS list image
 (yrss.hip scatter_count / image_layout / flush_image); groups feeding fewer
@@ -34,7 +34,7 @@ def dev():
                                  (64, 64, 1, 1), (254, 254, 1, 0), (300, 255, 1, 0)])
 @pytest.mark.parametrize("group", [32, 64])
 def test_count_mode_bucket_counts(dev, oracle_mod, cfg, group):
-    """10..256 buckets with count mode allowed for all (past ~100 buckets
+    """10..256 buckets with count mode allowed for all (past ~180 buckets
     the image and counters outgrow a wave's LDS share and the launch keeps
     the ballot path), both group sizes."""
     with _env(YRSS_GROUP_TILES=group, YRSS_COUNT_MAXNB=ANY_NB):

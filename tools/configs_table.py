@@ -18,12 +18,21 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 
 CONFIGS = [
-    ("1", "udp4_1flow", "64B UDP/IPv4, 1 flow (CPU-only config in BASELINE)"),
-    ("2", "udp4", "64B UDP/IPv4, 1M flows, burst 1024"),
-    ("3", "imix", "IMIX 64/570/1500 7:4:1 TCP+UDP, 1M flows"),
-    ("4", "vlan6_tcp", "64B VLAN+IPv6+TCP, 4M flows"),
-    ("5", "jumbo_tcp4", "9000B jumbo TCP/IPv4 (data_len 2048), 16M flows"),
-    ("-", "tcp4", "64B TCP/IPv4, 1M flows (all hashed)"),
+    ("1", "udp4_1flow", "64B UDP/IPv4, 1 flow (CPU-only config in BASELINE)", []),
+    ("2", "udp4", "64B UDP/IPv4, 1M flows, burst 1024", []),
+    ("3", "imix", "IMIX 64/570/1500 7:4:1 TCP+UDP, 1M flows", []),
+    ("4", "vlan6_tcp", "64B VLAN+IPv6+TCP, 4M flows", []),
+    ("5", "jumbo_tcp4", "9000B jumbo TCP/IPv4 (data_len 2048), 16M flows", []),
+    ("-", "tcp4", "64B TCP/IPv4, 1M flows (all hashed)", []),
+]
+# the same all-hashed stream over more dispatch queues (nb_procs lcores,
+# dispatch_only_core): each scatter path in turn (yrss.hip)
+QUEUES = [
+    ("q8", "tcp4", "64B TCP/IPv4, nb_procs 8 (9 buckets: few-bucket path)", ["--nb-procs", "8"]),
+    ("q16", "tcp4", "64B TCP/IPv4, nb_procs 16 (17 buckets: count mode)", ["--nb-procs", "16"]),
+    ("q32", "tcp4", "64B TCP/IPv4, nb_procs 32 (33 buckets: ranked)", ["--nb-procs", "32"]),
+    ("q64", "tcp4", "64B TCP/IPv4, nb_procs 64 (65 buckets: ballot, 2048-packet chunks)", ["--nb-procs", "64"]),
+    ("q255", "tcp4", "64B TCP/IPv4, nb_procs 255 (256 buckets: ballot)", ["--nb-procs", "255"]),
 ]
 
 
@@ -32,11 +41,13 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "configs.json"))
+    ap.add_argument("--queues", type=int, default=1, help="also the nb_procs sweep (QUEUES)")
     args = ap.parse_args()
     rows = []
-    for cid, prof, desc in CONFIGS:
+    for cid, prof, desc, extra in CONFIGS + (QUEUES if args.queues else []):
         cmd = [sys.executable, str(ROOT / "bench.py"), "--profile", prof, "--steps",
-               str(args.steps), "--cpu-seconds", str(args.cpu_seconds), "--pcie", "0"]
+               str(args.steps), "--cpu-seconds", str(args.cpu_seconds if not extra else 0),
+               "--pcie", "0", *extra]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         line = next((ln for ln in r.stdout.splitlines() if ln.startswith("{")), None)
         if r.returncode != 0 or line is None:

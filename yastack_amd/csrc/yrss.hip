@@ -929,55 +929,58 @@ __device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const u
     }
 }
 
-// Image layout of a group's runs (count mode): bucket b's run [off[b],
-// off[b] + gcnt[b]) is placed at image lines of its own, aligned as its global
-// lines are, so image word w of those lines is global slot w - io (io = the
-// run's image line start minus its global line start).  icur[b] is the run's
-// first image slot; desc[L] = {io, a, e, 0} describes image line L by its
-// run [a, e).  Returns the image words used (a multiple of kImgLine; at most
-// the group's packets + 62 per bucket).
+// Image layout of a group's runs (count mode): the runs are packed in bucket
+// order, bucket b's run [off[b], off[b] + gcnt[b]) at image slots
+// [icur[b], icur[b] + gcnt[b]).  The flush works per piece: a global 128-byte
+// line's part inside one run, desc[p] = {image slot - global slot, run start,
+// run end, line}.  Returns the pieces: a run of c slots touches at most
+// (c + 31) / 32 + 1 lines, so at most the group's lines + two per bucket.
 __device__ __forceinline__ uint32_t image_layout(uint32_t nb, const uint32_t *off,
                                                  const uint32_t *gcnt, uint32_t *icur,
                                                  u32x4 *desc, uint32_t lane)
 {
-    uint32_t carry = 0;
+    uint32_t carry = 0, pcarry = 0;
     for (uint32_t b0 = 0; b0 < nb; b0 += kWave) {
         const uint32_t b = b0 + lane;
         const uint32_t cnt = b < nb ? gcnt[b] : 0u, a = b < nb ? off[b] : 0u;
-        const uint32_t span =
-            cnt ? (((a & (kImgLine - 1u)) + cnt + kImgLine - 1u) & ~(kImgLine - 1u)) : 0u;
-        const uint32_t x = wave_incl_scan(span, lane);
-        const uint32_t ib = carry + x - span;
+        const uint32_t L0 = a / kImgLine;
+        const uint32_t np = cnt ? (a + cnt - 1u) / kImgLine - L0 + 1u : 0u;
+        const uint32_t x = wave_incl_scan(cnt, lane), xp = wave_incl_scan(np, lane);
+        const uint32_t ib = carry + x - cnt, pb = pcarry + xp - np;
         if (b < nb)
-            icur[b] = ib + (a & (kImgLine - 1u));
-        const u32x4 d = {ib - (a & ~(kImgLine - 1u)), a, a + cnt, 0u};
-        for (uint32_t L = ib / kImgLine; L < (ib + span) / kImgLine; ++L)
-            desc[L] = d;
+            icur[b] = ib;
+        const u32x4 d = {ib - a, a, a + cnt, 0u};
+        for (uint32_t k = 0; k < np; ++k) {
+            u32x4 e = d;
+            e[3] = L0 + k;
+            desc[pb + k] = e;
+        }
         carry += __shfl(x, kWave - 1, kWave);
+        pcarry += __shfl(xp, kWave - 1, kWave);
     }
-    return carry;
+    return pcarry;
 }
 
-// Writes a group's image (image_layout) out: each lane takes 16 bytes of an
-// image line.  Lines wholly inside their run leave as 16-byte non-temporal
-// stores; the partial lines at a run's ends are shared with the neighbouring
-// groups' runs and go out as plain 4-byte stores, merged in L2.
+// Writes a group's image (image_layout) out, a piece per 8 lanes, 16 bytes a
+// lane.  Pieces that are whole lines leave as 16-byte non-temporal stores;
+// the partial lines at a run's ends are shared with the neighbouring groups'
+// runs and go out as plain 4-byte stores, merged in L2.
 __device__ __forceinline__ void flush_image(const ScatterParams &P, const uint32_t *img,
-                                            const u32x4 *desc, uint32_t words, uint32_t lane)
+                                            const u32x4 *desc, uint32_t pieces, uint32_t lane)
 {
 #pragma unroll 2
-    for (uint32_t v = lane; v < words / 4u; v += kWave) {
-        const uint32_t w = 4u * v;
-        const u32x4 d = desc[w / kImgLine];
-        const u32x4 x = *reinterpret_cast<const u32x4 *>(img + w);
-        const uint32_t g = w - d[0], gl = g & ~(kImgLine - 1u);
+    for (uint32_t v = lane; v < pieces * 8u; v += kWave) {
+        const u32x4 d = desc[v / 8u];
+        const uint32_t gl = d[3] * kImgLine, g = gl + 4u * (v & 7u);
+        const uint32_t *src = img + (g + d[0]);
         if (gl >= d[1] && gl + kImgLine <= d[2]) {
+            const u32x4 x = {src[0], src[1], src[2], src[3]};
             __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(P.qidx + g));
         } else {
 #pragma unroll
             for (uint32_t k = 0; k < 4u; ++k)
                 if (g + k >= d[1] && g + k < d[2])
-                    P.qidx[g + k] = x[k];
+                    P.qidx[g + k] = src[k];
         }
     }
 }
@@ -1283,7 +1286,6 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
         wave_lds_sync();
         if constexpr (M > 0) {
             if (kseg > P.kmin) {
-                // the host sized the image for the group + 62 words per bucket
                 u32x4 *desc = reinterpret_cast<u32x4 *>(img + P.img);
                 const uint32_t words = image_layout(P.nb, off, gcnt, icur, desc, lane);
                 wave_lds_sync();
@@ -2209,7 +2211,7 @@ struct yrss_ctx {
     };
     std::vector<Occ> occ;           // resident_blocks cache
     uint32_t count_kmin = kFewBuckets;   // YRSS_COUNT_KMIN: count mode above this many buckets
-    uint32_t count_max_nb = 17;     // YRSS_COUNT_MAXNB: count mode up to this many buckets
+    uint32_t count_max_nb = 25;     // YRSS_COUNT_MAXNB: count mode up to this many buckets
     uint32_t scatter_wpb = 0;       // YRSS_SCATTER_WPB: waves per scatter workgroup (0: auto)
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
@@ -2371,11 +2373,11 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     // scatter groups: 2048 packets for the few-bucket LDS image path (nb <=
     // 8: a 9-10 KB image per wave, 3-4 workgroups per CU; 4096 had half the
     // occupancy, 1024 left more partial list lines dirty:
-    // profiles/r02_v10_group_ab.log), count mode (10..17 buckets) and the
-    // ballot path past 65 buckets; 4096 for the ranked path (18..65 buckets,
+    // profiles/r02_v10_group_ab.log), count mode (10..25 buckets) and the
+    // ballot path past 65 buckets; 4096 for the ranked path (26..65 buckets,
     // r01_v5_scatter_sweep.log, profiles/r02_v11_count_sweep.log)
     const uint64_t gt = c->group_tiles ? c->group_tiles
-                                       : (c->nb <= 17u || c->nb > 65u ? 32u : 64u);
+                                       : (c->nb <= c->count_max_nb || c->nb > 65u ? 32u : 64u);
     Layout L;
     L.ct_shift = ct_shift;
     L.shift = 0;
@@ -2392,16 +2394,21 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
 }
 
 // LDS of one scatter wave: its cursors (aux words), the group's list image
-// (img words, 0 = none) and, in count mode (cnt_off != 0), the image's line
+// (img words, 0 = none) and, in count mode (cnt_off != 0), the image's piece
 // descriptors and the lanes' counters; wpb waves per workgroup, halved until
 // a workgroup holds at most 64 KiB.  m: count mode's packets per lane (0 =
-// off).  A few-bucket image holds the group plus two lines per bucket up to
-// kFewBuckets; a count-mode one two lines for every bucket, image_layout's
-// bound.
+// off).  The image holds a few-bucket group's runs with two lines of slack
+// per bucket (few_img), which also holds a count-mode group's packed runs.
 struct ScatterLds {
     uint32_t aux, img, wlds, wpb, cnt_off, m;
 };
 constexpr uint32_t kScatterLdsMax = 64u * 1024u / 4u;   // words per workgroup
+
+// the few-bucket path's image: the group plus two lines of slack per bucket
+uint32_t few_img(const Layout &lay, uint32_t nb)
+{
+    return lay.seg + 2u * kImgLine * std::min(nb, kFewBuckets);
+}
 
 void scatter_wpb(const yrss_ctx *c, ScatterLds &r)
 {
@@ -2410,10 +2417,10 @@ void scatter_wpb(const yrss_ctx *c, ScatterLds &r)
         r.wpb /= 2;
 }
 
-// Count mode: for 10..count_max_nb (17) buckets by default.  With 9 the
+// Count mode: for 10..count_max_nb (25) buckets by default.  With 9 the
 // groups rarely feed more than 8 (nb_procs 8 with dispatch_only_core hashes
 // to 7 queues), and count mode's larger LDS share and unused q loads cost the
-// few-bucket path 8 %; past 17 buckets the ranked path is as fast or faster
+// few-bucket path 8 %; past 25 buckets the ranked path is as fast or faster
 // (runs of a line or two leave the image's whole-line stores little to do:
 // profiles/r02_v11_count_sweep.log).  It needs 32 or 64 packets per lane and
 // its image and counters within one wave's LDS share.
@@ -2426,8 +2433,8 @@ ScatterLds count_lds(const yrss_ctx *c, const Layout &lay)
         return r;
     r.m = lay.seg / kWave;
     r.aux = (4u * nb + 3u) & ~3u;
-    r.img = lay.seg + 2u * kImgLine * nb;
-    r.cnt_off = r.aux + r.img + r.img / kImgLine * 4u;
+    r.img = few_img(lay, nb);   // also the few-bucket groups' image (>= the packed runs)
+    r.cnt_off = r.aux + r.img + (lay.seg / kImgLine + 2u * nb) * 4u;   // image_layout's pieces
     r.wlds = (r.cnt_off + kCntStride * nb + 3u) & ~3u;
     if (r.wlds > kScatterLdsMax)
         return ScatterLds{};
@@ -2444,7 +2451,7 @@ ScatterLds scatter_lds(const yrss_ctx *c, const Layout &lay, bool ranked)
     } else {
         r.aux = (4u * nb + 3u) & ~3u;
         if (!c->no_img && lay.seg <= kImgPkts)
-            r.img = lay.seg + 2u * kImgLine * std::min(nb, kFewBuckets);
+            r.img = few_img(lay, nb);
         r.wlds = r.aux + r.img;
     }
     scatter_wpb(c, r);
