@@ -35,4 +35,5 @@ done
 step configs 900 python tools/configs_table.py --steps 50 --cpu-seconds 5 || exit 1
 step worker_soak 300 python tools/worker_soak.py --seconds 30 || exit 1
 step burst_soak 300 python tools/burst_soak.py --seconds 30 || exit 1
+step fanout_soak 300 python tools/fanout_soak.py --seconds 30 || exit 1
 echo "== done"
