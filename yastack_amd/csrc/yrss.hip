@@ -783,8 +783,9 @@ __device__ __forceinline__ void load_round(const int16_t *q, uint32_t r0, uint32
 // count of u below it (mbcnt), so ranking costs ~4 VALU per slot per bucket,
 // needs no LDS, and stores go straight from registers.  q of the next round is
 // in flight while a round is ranked.
-__device__ void scatter_few(const ScatterParams &P, const uint32_t *off, const uint32_t *gcnt,
-                            uint32_t beg, uint32_t end, uint32_t lane, uint32_t *img)
+__device__ __forceinline__ void scatter_few(const ScatterParams &P, const uint32_t *off,
+                                            const uint32_t *gcnt, uint32_t beg, uint32_t end,
+                                            uint32_t lane, uint32_t *img)
 {
     uint32_t ub[kFewBuckets], cur[kFewBuckets];
 #pragma unroll
@@ -1112,8 +1113,8 @@ __device__ __forceinline__ void scatter_count(const ScatterParams &P, const u32x
 // leader's value by ds_bpermute and add their rank inside the group.  Stores
 // go straight from registers.  A full round that is all one bucket (UDP
 // stretches) skips the ballots.
-__device__ void scatter_general(const ScatterParams &P, uint32_t *cur, uint32_t beg,
-                                uint32_t end, uint32_t lane)
+__device__ __forceinline__ void scatter_general(const ScatterParams &P, uint32_t *cur,
+                                                uint32_t beg, uint32_t end, uint32_t lane)
 {
     constexpr uint32_t kRound = kWave * kScatterRound;
     const uint64_t lt = lane_lt_mask(lane);
