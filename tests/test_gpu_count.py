@@ -97,3 +97,16 @@ def test_count_mode_unaligned(oracle_mod, qshift, ishift):
         qi_all = qi_buf.cpu().numpy()
         assert np.array_equal(qi_all[ishift:ishift + n].view(np.uint32), qi_ref)
         assert (qi_all[:ishift] == -1).all() and (qi_all[ishift + n:] == -1).all()
+
+
+@pytest.mark.parametrize("cfg", [(20, 20, 1, 0), (32, 32, 1, 1), (48, 48, 1, 0)])
+@pytest.mark.parametrize("n", [1025, 4097, 400003])
+@pytest.mark.parametrize("img", [0, 1])
+def test_ranked_image(dev, oracle_mod, cfg, n, img):
+    """The ranked path (18..65 buckets with count mode held to 17) with its
+    lists built in a packed LDS image (YRSS_RANK_IMG=1; the default up to 33
+    buckets) or through the per-chunk stage (0): the same FIFO lists."""
+    with _env(YRSS_RANK_IMG=img, YRSS_COUNT_MAXNB=17):
+        with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            for profile in (abi.SYN_TCP4, abi.SYN_FUZZ):
+                check(eng, oracle_mod, cfg, profile, n, first=n + 3)

@@ -60,6 +60,7 @@ constexpr uint32_t kRankStage = 1024;   // ranked scatter: chunk stage (packets)
 constexpr uint32_t kImgPkts = 4096;     // few-bucket scatter: largest group built in LDS
 constexpr uint32_t kImgLine = 32;       // entries per 128-byte line
 constexpr uint32_t kCntStride = 65;     // count mode: words per bucket's lane counters
+constexpr uint32_t kRankImgMaxNb = 33;  // ranked scatter: LDS image up to this many buckets
 // Toeplitz key tables: the 96 tuple bits are cut into fields of kHashBits
 // (MSB first); table t maps a field value to the XOR of the key windows its
 // set bits select.  8: 12 byte tables of 256 words (12 lookups; random indices
@@ -1357,6 +1358,58 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterPara
 
     const uint32_t c0 = gw << P.gshift;
     const uint32_t c1 = min(c0 + (1u << P.gshift), P.nchunk);
+    if (P.img) {
+        // The group's lists are built in a packed LDS image (image_layout)
+        // and leave through flush_image.  A packet's image slot is its
+        // bucket's run start in the image, plus the bucket's packets in the
+        // group's earlier chunks, plus its rank: no stage and no atomics.
+        if (c0 >= c1)
+            return;
+        uint32_t *goff = lst, *gcnt = goff + P.nb, *icur = gcnt + P.nb;
+        uint32_t *img = wbase + P.aux;
+        u32x4 *desc = reinterpret_cast<u32x4 *>(img + P.img);
+        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+            const uint32_t b = b0 + lane;
+            if (b < P.nb) {
+                const uint32_t *row = P.seg_off + (size_t)b * P.ncol;
+                const uint32_t o0 = row[c0], o1 = c1 < P.nchunk ? row[c1] : P.totals[b];
+                goff[b] = start[b] + o0;
+                gcnt[b] = o1 - o0;
+            }
+        }
+        wave_lds_sync();
+        const uint32_t pieces = image_layout(P.nb, goff, gcnt, icur, desc, lane);
+        wave_lds_sync();
+        for (uint32_t c = c0; c < c1; ++c) {
+            for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+                const uint32_t b = b0 + lane;
+                if (b < P.nb)   // the run's image start + the bucket's packets before chunk c
+                    cur[b] = icur[b] + start[b] + P.seg_off[(size_t)b * P.ncol + c] - goff[b];
+            }
+            wave_lds_sync();
+            const uint32_t pb = c * P.chunk;
+            const uint32_t pe = (uint64_t)pb + P.chunk < P.n ? pb + P.chunk : P.n;
+            for (uint32_t p0 = pb; p0 < pe; p0 += kWave * kScatterRound) {
+                int32_t qv[kScatterRound];
+                uint32_t rv[kScatterRound];
+#pragma unroll
+                for (int j = 0; j < kScatterRound; ++j) {
+                    const uint32_t pc = min(p0 + j * kWave + lane, pe - 1u);
+                    qv[j] = __builtin_nontemporal_load(P.q + pc);
+                    rv[j] = __builtin_nontemporal_load(P.rank + pc);
+                }
+#pragma unroll
+                for (int j = 0; j < kScatterRound; ++j) {
+                    const uint32_t p = p0 + j * kWave + lane;
+                    if (p < pe)
+                        img[cur[bucket_of((int16_t)qv[j], P.nq)] + rv[j]] = p;
+                }
+            }
+            wave_lds_sync();
+        }
+        flush_image(P, img, desc, pieces, lane);
+        return;
+    }
     for (uint32_t c = c0; c < c1; ++c) {
         // the chunk's cursor per bucket and its counting-sort layout: bucket b
         // holds stage slots [lst[b], lst[b] + count), count from the prefix
@@ -2206,6 +2259,8 @@ struct yrss_ctx {
     bool no_single = false;         // YRSS_NO_SINGLE: no grid-stride path for one-list batches
     bool no_count = false;          // YRSS_NO_COUNT: no count-mode scatter
     bool scatter_full = false;      // YRSS_SCATTER_FULL: a scatter wave per group
+    int rank_img = -1;              // YRSS_RANK_IMG: ranked scatter through an LDS image
+                                    // (1 on, 0 off, -1 up to kRankImgMaxNb buckets)
     struct Occ {
         const void *fn;
         uint32_t block, lds, blocks;
@@ -2448,7 +2503,21 @@ ScatterLds scatter_lds(const yrss_ctx *c, const Layout &lay, bool ranked)
     const uint32_t nb = c->nb;
     ScatterLds r{};
     if (ranked) {
-        r.wlds = 3u * nb + 2u * kRankStage;
+        // the packed image and its pieces, else the chunk stage.  The image
+        // gains up to 33 buckets: all-TCP +3 % at 29-33 (the next parse
+        // kernel 10-13 us faster, the scatter 1-4 us slower), IMIX even;
+        // from 37 buckets the scatter's loss is larger than the parse
+        // kernel's gain (profiles/r02_v11_count_sweep.log)
+        r.aux = (6u * nb + 3u) & ~3u;
+        r.img = lay.seg;
+        const uint32_t w = r.aux + r.img + (lay.seg / kImgLine + 2u * nb) * 4u;
+        const bool on = c->rank_img < 0 ? nb <= kRankImgMaxNb : c->rank_img > 0;
+        if (on && !c->no_img && w <= kScatterLdsMax) {
+            r.wlds = w;
+        } else {
+            r.aux = r.img = 0;
+            r.wlds = 3u * nb + 2u * kRankStage;
+        }
     } else {
         r.aux = (4u * nb + 3u) & ~3u;
         if (!c->no_img && lay.seg <= kImgPkts)
@@ -3023,6 +3092,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         if (v >= 1 && v <= YRSS_MAX_QUEUES + 1)
             c->count_max_nb = (uint32_t)v;
     }
+    if (const char *e = getenv("YRSS_RANK_IMG"))
+        c->rank_img = atoi(e) != 0 ? 1 : 0;
     if (const char *e = getenv("YRSS_SCATTER_FULL"))
         c->scatter_full = atoi(e) != 0;
     if (const char *e = getenv("YRSS_COUNT_KMIN")) {
@@ -3254,12 +3325,13 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     }
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
-    // 18..65 buckets (16-tile chunks): the parse kernel also emits each
-    // packet's rank in its chunk and the scatter counting-sorts each chunk in
-    // LDS.  Measured against the ballot scatter on one box: step -4 % at 33
-    // buckets, -2 % at 17; at 10 buckets (256-packet chunks) the ranks' cost in
-    // the parse kernel (+5-8 us) outweighed the gain, and chunks above
-    // kRankStage packets do not fit the stage.
+    // 18..65 buckets (16-tile chunks) not taken by count mode (26.. by
+    // default): the parse kernel also emits each packet's rank in its chunk
+    // and the scatter places it by that rank.  Measured against the ballot
+    // scatter on one box: step -4 % at 33 buckets, -2 % at 17; at 10 buckets
+    // (256-packet chunks) the ranks' cost in the parse kernel (+5-8 us)
+    // outweighed the gain, and chunks above kRankStage packets do not fit the
+    // stage.
     const ScatterLds cl = compact ? count_lds(c, lay) : ScatterLds{};
     const bool ranked =
         compact && !c->no_rank && !cl.cnt_off && c->nb > 17u && lay.chunk <= kRankStage;
