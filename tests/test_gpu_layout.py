@@ -76,7 +76,8 @@ def test_forced_layouts(dev, oracle_mod, chunk, group, profile):
 
 @pytest.mark.parametrize("cfg", [(32, 32, 1, 0), (100, 100, 1, 1), (17, 17, 1, 0)])
 def test_bucket_count_layouts(dev, oracle_mod, cfg):
-    """18..65 buckets get 16-tile chunks, more get 64 (count slots per wave)."""
+    """Past 17 buckets chunks are 16 tiles while the count slots per wave
+    hold them (yrss.hip layout_for), larger past that."""
     with SoftRss(*cfg, device=0, max_burst=0) as eng:
         for profile in (abi.SYN_TCP4, abi.SYN_IMIX):
             check(eng, oracle_mod, cfg, profile, 1 << 20, first=99)

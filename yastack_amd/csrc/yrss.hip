@@ -52,7 +52,7 @@ constexpr int kScatterBlock = 256;     // 4 waves (segments) per workgroup
 constexpr int kScatterWaves = kScatterBlock / kWave;
 constexpr int kMaxWavesPerCU = 32;
 constexpr uint32_t kMaxChunks = 65536;  // per launch; bounds the count matrix [nb][ncol]
-constexpr uint32_t kCntWords = 512;     // parse: per-wave LDS count slots (chunks x nb)
+constexpr uint32_t kCntWords = 2048;    // parse: per-wave LDS count slots (chunks x nb)
 constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
 constexpr int kScatterRound = 8;       // packets per lane per scatter round
 constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this many buckets
@@ -557,7 +557,7 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
 //   kFilter  also classify protocol_filter / KNI (one byte per packet)
 //   kNT      non-temporal (streaming) window loads
 //   kBlock   workgroup size (256/512): waves per CU, one key table per group
-// LDS: key tables 12 KiB | staging 4 KiB per wave | count slots 2 KiB per wave |
+// LDS: key tables 12 KiB | staging 4 KiB per wave | count slots 8 KiB per wave |
 //      output buffer 1.75 KiB per wave | KNI bitmaps 16 KiB (kFilter only).
 // ---------------------------------------------------------------------------
 template <int kCount, bool kFilter, bool kNT, int kBlock>
@@ -2420,7 +2420,10 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     const uint64_t slots = std::max<uint32_t>(1u, kCntWords / c->nb);
     const uint64_t max_chunks = std::min<uint64_t>(kMaxChunks, waves * slots);
     const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
-    uint64_t ct = c->chunk_tiles ? c->chunk_tiles : (c->nb <= 17u ? 4u : c->nb <= 65u ? 16u : 64u);
+    // 4 tiles up to 17 buckets, else 16 (1024 packets, the ranked path's
+    // stage); larger when the waves' count slots run out (at 2^24 packets
+    // from 257 buckets: 2048 slot words per wave, profiles/r02_v11_count_sweep.log)
+    uint64_t ct = c->chunk_tiles ? c->chunk_tiles : (c->nb <= 17u ? 4u : 16u);
     ct = std::max<uint64_t>(ct, (tiles + max_chunks - 1) / max_chunks);
     uint32_t ct_shift = 0;
     while ((1ull << ct_shift) < ct)
@@ -2429,9 +2432,9 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     // scatter groups: 2048 packets for the few-bucket LDS image path (nb <=
     // 8: a 9-10 KB image per wave, 3-4 workgroups per CU; 4096 had half the
     // occupancy, 1024 left more partial list lines dirty:
-    // profiles/r02_v10_group_ab.log), count mode (10..25 buckets) and the
-    // ballot path past 65 buckets; 4096 for the ranked path (26..65 buckets,
-    // r01_v5_scatter_sweep.log, profiles/r02_v11_count_sweep.log)
+    // profiles/r02_v10_group_ab.log), count mode (10..25 buckets) and past
+    // 65 buckets; 4096 for the ranked path at 26..65 buckets
+    // (r01_v5_scatter_sweep.log, profiles/r02_v11_count_sweep.log)
     const uint64_t gt = c->group_tiles ? c->group_tiles
                                        : (c->nb <= c->count_max_nb || c->nb > 65u ? 32u : 64u);
     Layout L;
@@ -3325,13 +3328,13 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     }
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
-    // 18..65 buckets (16-tile chunks) not taken by count mode (26.. by
-    // default): the parse kernel also emits each packet's rank in its chunk
-    // and the scatter places it by that rank.  Measured against the ballot
-    // scatter on one box: step -4 % at 33 buckets, -2 % at 17; at 10 buckets
-    // (256-packet chunks) the ranks' cost in the parse kernel (+5-8 us)
-    // outweighed the gain, and chunks above kRankStage packets do not fit the
-    // stage.
+    // Past 17 buckets with 16-tile chunks, when count mode does not take the
+    // batch (26..256 buckets by default): the parse kernel also emits each
+    // packet's rank in its chunk and the scatter places it by that rank.
+    // Measured against the ballot scatter: step -4 % at 33 buckets, -2 % at
+    // 17, +9 % at 129, +6 % at 256; at 10 buckets (256-packet chunks) the
+    // ranks' cost in the parse kernel (+5-8 us) outweighed the gain, and
+    // chunks above kRankStage packets do not fit the stage.
     const ScatterLds cl = compact ? count_lds(c, lay) : ScatterLds{};
     const bool ranked =
         compact && !c->no_rank && !cl.cnt_off && c->nb > 17u && lay.chunk <= kRankStage;
