@@ -3332,9 +3332,9 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     // batch (26..256 buckets by default): the parse kernel also emits each
     // packet's rank in its chunk and the scatter places it by that rank.
     // Measured against the ballot scatter: step -4 % at 33 buckets, -2 % at
-    // 17, +3 % at 65, +9 % at 129, even at 256; at 10 buckets (256-packet chunks) the
-    // ranks' cost in the parse kernel (+5-8 us) outweighed the gain, and
-    // chunks above kRankStage packets do not fit the stage.
+    // 17, +3 % at 65, +9 % at 129, even at 256; at 10 buckets (256-packet
+    // chunks) the ranks' cost in the parse kernel (+5-8 us) outweighed the
+    // gain, and chunks above kRankStage packets do not fit the stage.
     const ScatterLds cl = compact ? count_lds(c, lay) : ScatterLds{};
     const bool ranked =
         compact && !c->no_rank && !cl.cnt_off && c->nb > 17u && lay.chunk <= kRankStage;
