@@ -1175,11 +1175,11 @@ __device__ __forceinline__ void scatter_general(const ScatterParams &P, uint32_t
 // Kernel 3: stable scatter of packet indices into per-bucket lists.
 // Persistent: as many waves as are resident, wave w taking groups w, w + W,
 // ... (W waves; the waves in flight together cover one stretch of the batch,
-// as a wave per group did).  A wave works out the lists' starts once, and while it works on a
-// group the next group's bucket prefixes (and, in count mode, its q) are
-// already in flight: one wave per group paid those loads' latency once per
-// group (13 us of a 22 us all-TCP scatter at 2^24 packets, 25 us with 65
-// buckets, where LDS left two waves per CU).
+// as a wave per group did).  A wave works out the lists' starts once, and
+// while it works on a group the next group's bucket prefixes (and, in count
+// mode, its q) are already in flight: one wave per group paid those loads'
+// latency once per group (13 us of a 22 us all-TCP scatter at 2^24 packets,
+// 25 us with 65 buckets, where LDS left two waves per CU).
 // M > 0: groups of 64 * M packets feeding more than P.kmin buckets take
 // count mode.
 // ---------------------------------------------------------------------------
