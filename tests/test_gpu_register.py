@@ -64,3 +64,28 @@ def test_python_wrappers(dev, oracle_mod):
             assert np.array_equal(r.qidx, qi) and np.array_equal(r.qstart[: qs.size], qs)
         eng.worker_stop()
         eng.unregister_host_memory(pool.ctypes.data)
+
+
+@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (4, 2, 0, 1)])
+def test_registered_dispatcher_through_worker(dev, oracle_mod, cfg):
+    """A context with a resident worker serves each shim call as a one-packet
+    worker burst: same answers, frames from unregistered memory (the shim
+    copies each window into its own registered slot), lengths past the
+    80-byte window included."""
+    lib = abi.load()
+    frames = _frames(oracle_mod, 300, 700 + cfg[0])
+    q, _, _, _ = _expect(oracle_mod, frames, cfg)
+    fn = DISPATCH_FUNC_T(ctypes.cast(lib.yrss_toeplitz_dispatch, ctypes.c_void_p).value)
+    with SoftRss(*cfg, device=0) as eng:
+        eng.worker_start(4, 1)
+        assert lib.yrss_set_dispatch_ctx(eng._ctx) == 0
+        got = []
+        for j, f in enumerate(frames):
+            buf = ctypes.create_string_buffer(f, len(f))
+            got.append(fn(ctypes.cast(buf, ctypes.c_void_p), len(f), j % 7, cfg[1]))
+        assert np.array_equal(np.array(got, np.int16), q)
+        assert max(len(f) for f in frames) > 80
+        eng.worker_stop()
+        # without the worker the same context falls back to one launch per call
+        buf = ctypes.create_string_buffer(frames[0], len(frames[0]))
+        assert fn(ctypes.cast(buf, ctypes.c_void_p), len(frames[0]), 0, cfg[1]) == int(q[0])

@@ -249,6 +249,65 @@ static int run_fanout(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
     return 0;
 }
 
+/* The per-packet registration shim (yrss_toeplitz_dispatch through a
+ * dispatch_func_t pointer, as process_packets calls it, ff_dpdk_if.c:1078-1079),
+ * one packet at a time over the pool's frames: without a worker (a one-packet
+ * launch and a sync per call) and with one resident on the shim's context.
+ * Every answer is compared with the burst API's answer for the same packet. */
+typedef int (*dispatch_func_t)(void *data, uint16_t len, uint16_t queue_id, uint16_t nb_queues);
+
+static int run_shim(const struct yrss_config *cfg0, void **mbufs, uint32_t pool, double secs,
+                    uint32_t profile, const uint8_t **fdata, uint16_t *flen, int16_t *q_all)
+{
+    struct yrss_config cfg = *cfg0;
+    cfg.max_burst = 4096;
+    fill_frames(mbufs, pool, fdata, flen);
+    dispatch_func_t fn = yrss_toeplitz_dispatch;
+    for (int worker = 0; worker < 2; ++worker) {
+        yrss_ctx *ctx = NULL;
+        int rc;
+        if ((rc = yrss_init(&cfg, &ctx)) != 0) {
+            fprintf(stderr, "yrss_init: %d\n", rc);
+            return 2;
+        }
+        const uint32_t nref = pool < 4096u ? pool : 4096u;
+        if ((rc = yrss_dispatch_frames(ctx, fdata, flen, nref, q_all, NULL, NULL, NULL)) != 0 ||
+            (worker && (rc = yrss_worker_start(ctx, 4, 1)) != 0) ||
+            (rc = yrss_set_dispatch_ctx(ctx)) != 0) {
+            fprintf(stderr, "shim setup: %d\n", rc);
+            return 2;
+        }
+        for (uint32_t j = 0; j < 64; ++j)   /* warm up (first worker call registers its slot) */
+            (void)fn((void *)fdata[j], flen[j], 0, 3);
+        uint64_t calls = 0, bad = 0;
+        const double t0 = now();
+        double t1 = t0;
+        while (t1 - t0 < secs) {
+            const uint32_t j = (uint32_t)(calls % nref);
+            const int q = fn((void *)fdata[j], flen[j], 0, 3);
+            bad += q != q_all[j];
+            ++calls;
+            if ((calls & 255u) == 0)
+                t1 = now();
+        }
+        t1 = now();
+        printf("{\"tool\": \"yrss_cbench\", \"api\": \"yrss_toeplitz_dispatch\", "
+               "\"profile\": %u, \"worker\": %d, \"calls\": %llu, \"seconds\": %.3f, "
+               "\"us_per_call\": %.2f, \"mpps\": %.4f, \"mismatches\": %llu, \"mode\": 6, "
+               "\"note\": \"per-packet registration shim through a dispatch_func_t pointer; "
+               "%s\"}\n",
+               profile, worker, (unsigned long long)calls, t1 - t0, (t1 - t0) / calls * 1e6,
+               calls / (t1 - t0) / 1e6, (unsigned long long)bad,
+               worker ? "one-packet bursts of a resident worker" : "one launch + sync per packet");
+        fflush(stdout);
+        yrss_set_dispatch_ctx(NULL);
+        yrss_fini(ctx);
+        if (bad)
+            return 4;
+    }
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     const uint32_t profile = argc > 1 ? (uint32_t)atoi(argv[1]) : YRSS_SYN_UDP4;
@@ -432,6 +491,11 @@ int main(int argc, char **argv)
             if (burst_arg)
                 break;
         }
+    if (mode_env && strchr(mode_env, '6')) {
+        const int rc = run_shim(&cfg, mbufs, pool, secs, profile, fdata, flen, q_all);
+        if (rc)
+            return rc;
+    }
     free(arena);
     return 0;
 }

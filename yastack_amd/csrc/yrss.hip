@@ -2351,6 +2351,8 @@ struct yrss_ctx {
             uint8_t copy;          // bit k: output k comes from the slot's staging
         } *out = nullptr;          // [nslots]
     } w;
+    // yrss_toeplitz_dispatch through the worker: one registered window slot
+    uint8_t *shim_win = nullptr;
     // The compaction workspace is shared by every dispatch of the context; a
     // dispatch on a different stream than the previous one first waits for
     // the work queued on that stream (recorded at the switch, so same-stream
@@ -3225,6 +3227,7 @@ void yrss_fini(yrss_ctx *c)
     (void)hipHostFree(c->h_done);
     for (uint32_t r = 0; r < c->nranges; ++r)
         host_reg_release(c->range_base[r]);
+    free(c->shim_win);
     if (c->switch_ev)
         (void)hipEventDestroy(c->switch_ev);
     if (c->stream)
@@ -3495,11 +3498,49 @@ int yrss_set_dispatch_ctx(yrss_ctx *c)
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
+                  int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                  uint32_t flags, uint64_t *ticket);
+
+// The shim's packet as a one-packet burst of the context's resident worker:
+// its window (the at most YRSS_WIN_FULL bytes the GPU reads) is copied into a
+// slot the context registers on first use, so the caller's mbuf need not lie
+// in registered memory.  No HIP call per packet: a submit and a spin on the
+// burst's completion word.
+int shim_worker(yrss_ctx *c, const uint8_t *d, uint16_t len)
+{
+    if (!c->shim_win) {
+        void *m = aligned_alloc(4096, 4096);
+        if (!m)
+            return -1;
+        if (yrss_register_host_memory(c, m, 4096) != 0) {
+            free(m);
+            return -1;
+        }
+        c->shim_win = static_cast<uint8_t *>(m);
+    }
+    memcpy(c->shim_win, d, len < YRSS_WIN_FULL ? len : YRSS_WIN_FULL);
+    const uint8_t *p = c->shim_win;
+    int16_t q = 0;
+    uint64_t t = 0;
+    if (worker_submit(c, &p, &len, 1u, &q, nullptr, nullptr, nullptr, kWorkerFrames, &t) != 0 ||
+        yrss_worker_poll(c, t, 1) != 0)
+        return -1;
+    return q;
+}
+}  // namespace
+
+extern "C" {
+
 // toeplitz_dispatch's own signature (ff_dpdk_if.c:1945-1946), so it can be
-// handed to ff_regist_packet_dispatcher unchanged.  Each call is a one-packet
-// burst through the GPU (yrss_burst_small), bit-identical to the reference,
-// but it pays a launch and a synchronisation per packet: the burst hook is
-// the fast path.  queue_id and nb_queues are unused, as in the reference.
+// handed to ff_regist_packet_dispatcher unchanged.  Bit-identical to the
+// reference.  A context with a resident worker (yrss_worker_start) serves
+// each call as a one-packet worker burst; otherwise each call is a one-packet
+// launch (yrss_burst_small) and a synchronisation.  Either way the burst hook
+// is the fast path.  queue_id and nb_queues are unused, as in the reference.
 int yrss_toeplitz_dispatch(void *data, uint16_t len, uint16_t queue_id, uint16_t nb_queues)
 {
     (void)queue_id;
@@ -3516,6 +3557,8 @@ int yrss_toeplitz_dispatch(void *data, uint16_t len, uint16_t queue_id, uint16_t
         return -1;
     }
     const uint8_t *d = static_cast<const uint8_t *>(data);
+    if (c->w.on)
+        return shim_worker(c, d, len);
     int16_t q = 0;
     if (yrss_dispatch_frames(c, &d, &len, 1u, &q, nullptr, nullptr, nullptr) != 0)
         return -1;
