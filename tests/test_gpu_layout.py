@@ -140,3 +140,16 @@ def test_unaligned_list_outputs(oracle_mod, profile, shift):
         qi_all = qi_buf.cpu().numpy()
         assert np.array_equal(qi_all[shift:shift + n].view(np.uint32), qi_ref)
         assert (qi_all[:shift] == -1).all() and (qi_all[shift + n:] == -1).all()   # no overrun
+
+
+@pytest.mark.parametrize("xcd", [0, 1])
+@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (8, 8, 1, 0), (16, 16, 1, 0), (64, 64, 1, 1),
+                                 (255, 255, 1, 0)])
+def test_scatter_xcd_mapping(dev, oracle_mod, cfg, xcd):
+    """YRSS_SCATTER_XCD moves scatter groups between workgroups (XCD-contiguous
+    or round-robin; default by bucket count): every path's lists are the same,
+    including ragged grids (n not a multiple of a group)."""
+    with _env(YRSS_SCATTER_XCD=xcd):
+        with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            for profile in (abi.SYN_TCP4, abi.SYN_FUZZ):
+                check(eng, oracle_mod, cfg, profile, 777777, first=31)

@@ -132,9 +132,24 @@ struct ScatterParams {
     uint32_t wlds;             // words of LDS per wave
     uint32_t cnt_off;          // count mode: wave LDS word offset of its counters (0: off)
     uint32_t kmin;             // count mode for groups feeding more than kmin buckets
+    uint32_t xcd;              // workgroups of one XCD take consecutive groups (xcd_block)
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Workgroup b runs on XCD b mod 8, each XCD with its own L2.  With `on`, the
+// workgroups of one XCD take one contiguous range of logical blocks (a
+// bijection for any grid size), so the scatter groups that share a list
+// line at a run boundary are written through the same L2, where the two
+// partial writes merge into one line before it leaves for HBM.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t on)
+{
+    const uint32_t b = blockIdx.x, nb = gridDim.x;
+    if (!on || nb < 16u)
+        return b;
+    const uint32_t per = nb >> 3, rem = nb & 7u, x = b & 7u;
+    return x * per + min(x, rem) + (b >> 3);
+}
 
 // orders a wave's LDS accesses across lanes (all lanes of one wave)
 __device__ __forceinline__ void wave_lds_sync()
@@ -1199,7 +1214,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     uint32_t *icur = gcnt + P.nb;
     uint32_t *img = start + P.aux;
     const uint32_t W = gridDim.x * (blockDim.x / kWave);
-    const uint32_t gw = blockIdx.x * (blockDim.x / kWave) + wave;
+    const uint32_t gw = xcd_block(P.xcd) * (blockDim.x / kWave) + wave;
     const uint32_t ng = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
     auto bounds = [&](uint32_t g, uint32_t &beg, uint32_t &end) {
         beg = g * P.seg;
@@ -1338,7 +1353,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterPara
     uint32_t *lst = cur + P.nb;
     uint32_t *sidx = lst + P.nb;
     uint32_t *sbk = sidx + kRankStage;
-    const uint32_t gw = blockIdx.x * (blockDim.x / kWave) + wave;
+    const uint32_t gw = xcd_block(P.xcd) * (blockDim.x / kWave) + wave;
 
     uint32_t carry = 0;
     for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
@@ -2269,6 +2284,7 @@ struct yrss_ctx {
     uint32_t count_kmin = kFewBuckets;   // YRSS_COUNT_KMIN: count mode above this many buckets
     uint32_t count_max_nb = 25;     // YRSS_COUNT_MAXNB: count mode up to this many buckets
     uint32_t scatter_wpb = 0;       // YRSS_SCATTER_WPB: waves per scatter workgroup (0: auto)
+    int scatter_xcd = -1;           // YRSS_SCATTER_XCD: XCD-contiguous scatter groups (-1: auto)
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
     uint32_t *d_scan_fault = nullptr;   // host-coherent pinned word (yrss_status)
@@ -3111,6 +3127,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         if (v == 1 || v == 2 || v == 4)
             c->scatter_wpb = (uint32_t)v;
     }
+    if (const char *e = getenv("YRSS_SCATTER_XCD"))
+        c->scatter_xcd = atoi(e) != 0 ? 1 : 0;
     if (const char *e = getenv("YRSS_GROUP_TILES")) {
         const int v = atoi(e);
         if (v >= 1 && v <= 65536)
@@ -3420,6 +3438,14 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.wlds = sl.wlds;
     S.cnt_off = sl.cnt_off;
     S.kmin = c->count_kmin;
+    // XCD-contiguous groups from 10 buckets (count mode and the ranked
+    // paths): the L2 merges the run-boundary lines that neighbouring groups
+    // share, so fewer partial lines are written back, most of them inside
+    // the next parse kernel.  All-TCP step on one box: +3 % at 17 buckets,
+    // +2 % at 33, -1 % at 65, +1 % at 129, +5 % at 256; the few-bucket path
+    // (9 buckets) lost 1.5 %, UDP/TCP at 4 buckets even
+    // (profiles/r02_v15_xcd_ab.log)
+    S.xcd = c->scatter_xcd >= 0 ? (uint32_t)c->scatter_xcd : (c->nb >= 10u ? 1u : 0u);
     {
         void (*fn)(ScatterParams) = ranked          ? yrss_scatter_ranked
                                     : sl.m == 64u ? yrss_scatter<64>
