@@ -143,8 +143,8 @@ def test_unaligned_list_outputs(oracle_mod, profile, shift):
 
 
 @pytest.mark.parametrize("xcd", [0, 1])
-@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (8, 8, 1, 0), (16, 16, 1, 0), (64, 64, 1, 1),
-                                 (255, 255, 1, 0)])
+@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (8, 8, 1, 0), (16, 16, 1, 0), (48, 48, 1, 0),
+                                 (64, 64, 1, 1), (255, 255, 1, 0)])
 def test_scatter_xcd_mapping(dev, oracle_mod, cfg, xcd):
     """YRSS_SCATTER_XCD moves scatter groups between workgroups (XCD-contiguous
     or round-robin; default by bucket count): every path's lists are the same,

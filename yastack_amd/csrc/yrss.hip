@@ -60,7 +60,8 @@ constexpr uint32_t kRankStage = 1024;   // ranked scatter: chunk stage (packets)
 constexpr uint32_t kImgPkts = 4096;     // few-bucket scatter: largest group built in LDS
 constexpr uint32_t kImgLine = 32;       // entries per 128-byte line
 constexpr uint32_t kCntStride = 65;     // count mode: words per bucket's lane counters
-constexpr uint32_t kRankImgMaxNb = 33;  // ranked scatter: LDS image up to this many buckets
+constexpr uint32_t kRankImgMaxNb = 65;  // ranked scatter: LDS image up to this many buckets
+constexpr uint32_t kRankImgMaxNbRr = 33; // the same with round-robin (not XCD-contiguous) groups
 // Toeplitz key tables: the 96 tuple bits are cut into fields of kHashBits
 // (MSB first); table t maps a field value to the XOR of the key windows its
 // set bits select.  8: 12 byte tables of 256 words (12 lookups; random indices
@@ -2275,7 +2276,7 @@ struct yrss_ctx {
     bool no_count = false;          // YRSS_NO_COUNT: no count-mode scatter
     bool scatter_full = false;      // YRSS_SCATTER_FULL: a scatter wave per group
     int rank_img = -1;              // YRSS_RANK_IMG: ranked scatter through an LDS image
-                                    // (1 on, 0 off, -1 up to kRankImgMaxNb buckets)
+                                    // (1 on, 0 off, -1 up to kRankImgMaxNb[Rr] buckets)
     struct Occ {
         const void *fn;
         uint32_t block, lds, blocks;
@@ -2487,6 +2488,17 @@ uint32_t few_img(const Layout &lay, uint32_t nb)
     return lay.seg + 2u * kImgLine * std::min(nb, kFewBuckets);
 }
 
+// XCD-contiguous scatter groups from 10 buckets (count mode and the ranked
+// paths): the L2 merges the run-boundary lines that neighbouring groups
+// share, so fewer partial lines are written back, most of them inside the
+// next parse kernel.  All-TCP step on one box: +3 % at 17 buckets, +2 % at
+// 33, -1 % at 65, +1 % at 129, +5 % at 256; the few-bucket path (9 buckets)
+// lost 1.5 %, UDP/TCP at 4 buckets even (profiles/r02_v15_xcd_ab.log).
+bool scatter_xcd_on(const yrss_ctx *c)
+{
+    return c->scatter_xcd >= 0 ? c->scatter_xcd != 0 : c->nb >= 10u;
+}
+
 void scatter_wpb(const yrss_ctx *c, ScatterLds &r)
 {
     r.wpb = c->scatter_wpb ? c->scatter_wpb : (uint32_t)kScatterWaves;
@@ -2532,7 +2544,11 @@ ScatterLds scatter_lds(const yrss_ctx *c, const Layout &lay, bool ranked)
         r.aux = (6u * nb + 3u) & ~3u;
         r.img = lay.seg;
         const uint32_t w = r.aux + r.img + (lay.seg / kImgLine + 2u * nb) * 4u;
-        const bool on = c->rank_img < 0 ? nb <= kRankImgMaxNb : c->rank_img > 0;
+        // With XCD-contiguous groups the image pays up to 65 buckets (all-TCP
+        // step +2..6 % at 49, +0.5..2 % at 65; -4 % at 129, -13 % at 256:
+        // profiles/r02_v16_rankimg_xcd_ab.log); round-robin, up to 33.
+        const uint32_t img_max = scatter_xcd_on(c) ? kRankImgMaxNb : kRankImgMaxNbRr;
+        const bool on = c->rank_img < 0 ? nb <= img_max : c->rank_img > 0;
         if (on && !c->no_img && w <= kScatterLdsMax) {
             r.wlds = w;
         } else {
@@ -3438,14 +3454,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.wlds = sl.wlds;
     S.cnt_off = sl.cnt_off;
     S.kmin = c->count_kmin;
-    // XCD-contiguous groups from 10 buckets (count mode and the ranked
-    // paths): the L2 merges the run-boundary lines that neighbouring groups
-    // share, so fewer partial lines are written back, most of them inside
-    // the next parse kernel.  All-TCP step on one box: +3 % at 17 buckets,
-    // +2 % at 33, -1 % at 65, +1 % at 129, +5 % at 256; the few-bucket path
-    // (9 buckets) lost 1.5 %, UDP/TCP at 4 buckets even
-    // (profiles/r02_v15_xcd_ab.log)
-    S.xcd = c->scatter_xcd >= 0 ? (uint32_t)c->scatter_xcd : (c->nb >= 10u ? 1u : 0u);
+    S.xcd = scatter_xcd_on(c) ? 1u : 0u;
     {
         void (*fn)(ScatterParams) = ranked          ? yrss_scatter_ranked
                                     : sl.m == 64u ? yrss_scatter<64>
