@@ -57,3 +57,23 @@ def test_shared_device_refused():
     r = _run(["--gpus", "2", "--dry", "--steps", "1"], {"YRSS_BENCH_FAKE_SAME_DEVICE": "1"})
     assert r.returncode != 0
     assert "share a device" in r.stderr
+
+
+def test_torchrun_two_ranks():
+    """The driver's form for N > 1: torch.distributed.run sets WORLD_SIZE /
+    RANK / LOCAL_RANK and bench.py runs as one of its ranks."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in DIST_VARS}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "2",
+                        "--dry", "--steps", "2", "--warmup", "0", "--pkts", "500"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and len(set(d["config"]["devices"])) == 2
+    assert d["pkts_total"] == 2 * 2 * 500
