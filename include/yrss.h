@@ -280,8 +280,11 @@ int yrss_dispatch_frames(yrss_ctx *ctx, const uint8_t *const *data,
  * burst with its own launch and synchronisation (10.8 µs per call measured);
  * if the context has a resident worker (yrss_worker_start), the call is a
  * one-packet worker burst instead, no HIP call (9.3 µs; the window is copied
- * into a slot the context registers on first use).  A drop-in for
- * registration, not the fast path — use the burst hook or the worker.
+ * into a slot the context registers on first use; the shim then shares that
+ * worker's ring, so submit nothing else to the context while shim calls run:
+ * a slot still holding an unpolled ticket makes the call return -1).  A
+ * drop-in for registration, not the fast path — use the burst hook or the
+ * worker.
  * Calls from several threads (soft_dispatch=0 runs the dispatcher on every
  * lcore, ff_dpdk_if.c:1653) are serialised by one process-wide mutex.  Give the
  * shim a context of its own: while that context has a YRSS_F_ASYNC burst
