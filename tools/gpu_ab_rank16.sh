@@ -1,6 +1,9 @@
 # Ranks as 16-byte stores (default build, YRSS_RANK16=1) vs per-lane 2-byte
 # stores (build/r16_0: -DYRSS_RANK16=0), ranked paths on all-TCP; the ranked
-# GPU tests on the default build first.
+# GPU tests on the default build first.  The YRSS_RANK16 branch (flush_out's
+# kRank part writing a whole tile batch as one raw_buffer_store_b128 per lane,
+# exactly as its q part does) was measured and not kept, so this script no
+# longer has two variants to compare.
 #   mkdir -p build/r16_0; hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DYRSS_RANK16=0 \
 #     -I include yastack_amd/csrc/yrss.hip yastack_amd/csrc/yrss_pcap.cpp yastack_amd/csrc/yrss_shard.cpp \
 #     yastack_amd/csrc/yrss_fanout.cpp -o build/r16_0/libyrss.so
