@@ -288,10 +288,11 @@ def cpu_baseline(args, nb_queues):
     }
 
 
-def probe_traffic(batches, n, stride, steps):
+def probe_traffic(batches, n, stride, steps, mode=0):
     """Average duration of the ideal-traffic twin (tools/yrss_probe.hip) over
     the same buffers, rotated like the timed steps: the practical floor of the
-    parse kernel on this box."""
+    parse kernel on this box (mode 0).  Mode 1 moves only its reads (66 B/pkt):
+    the box's streaming-read rate for the same shape."""
     import ctypes
 
     import torch
@@ -300,12 +301,12 @@ def probe_traffic(batches, n, stride, steps):
     if stride != 64 or not lib_path.exists():
         return None
     lib = ctypes.CDLL(str(lib_path))
-    fn = lib.yrss_probe_traffic_launch
+    fn = lib.yrss_probe_traffic_launch_mode
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32, ctypes.c_void_p]
+    fn.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
     stream = torch.cuda.current_stream()
     args = [(w.data_ptr(), ln.data_ptr(), o.q.data_ptr(), o.hash.data_ptr(), n,
-             stream.cuda_stream) for w, ln, o in batches]
+             stream.cuda_stream, mode) for w, ln, o in batches]
     for i in range(3):
         fn(*args[i % len(args)])
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -503,6 +504,7 @@ def main(argv=None):
         eng.dispatch_dev(w_k, l_k, args.stride, n, out=o_k, compact=not args.no_compact)
 
     probe_s = probe_traffic(batches, n, args.stride, max(args.steps, 10))
+    probe_rd_s = probe_traffic(batches, n, args.stride, max(args.steps, 10), mode=1)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -624,7 +626,10 @@ def main(argv=None):
                     "what": "ideal-traffic twin (tools/yrss_probe.hip): same bytes, no parse",
                     "us": round(probe_s * 1e6, 2),
                     "achieved": round(bpp * n / probe_s / 1e9, 1),
-                    "parse_frac_of_probe": round(probe_s / k_avg_s, 4) if k_avg_s else None},
+                    "parse_frac_of_probe": round(probe_s / k_avg_s, 4) if k_avg_s else None,
+                    "reads_only_us": round(probe_rd_s * 1e6, 2) if probe_rd_s else None,
+                    "reads_only_achieved": round((bpp - 6) * n / probe_rd_s / 1e9, 1)
+                    if probe_rd_s and not args.filter else None},
             },
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,

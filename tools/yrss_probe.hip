@@ -101,10 +101,142 @@ __global__ __launch_bounds__(512) void yrss_probe_traffic(const u32x4 *win, cons
     }
 }
 
+// Write-phase experiment: the same traffic as mode 0, but each wave keeps the
+// outputs of up to `cap` chunks (kB max) in LDS and writes them only when its
+// buffer is full or, with kClock, when the chip-wide 100 MHz clock
+// (s_memrealtime) enters a new period of `period` ticks -- so every wave's
+// writes land in the same short window and the memory controllers see write
+// bursts between long read phases instead of a trickle of writes.
+constexpr uint32_t kB = 4;
+template <bool kClock>
+__global__ __launch_bounds__(512) void yrss_probe_phase(const u32x4 *win, const uint16_t *len,
+                                                        int16_t *q, uint32_t *hash, uint32_t n,
+                                                        uint32_t period, uint32_t cap)
+{
+    __shared__ u32x4 st[kWaves][256];
+    __shared__ __attribute__((aligned(16))) uint32_t hb[kWaves][kB * kC * 64];
+    __shared__ __attribute__((aligned(16))) uint16_t qb[kWaves][kB * kC * 64];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t W = gridDim.x * kWaves;
+    const uint32_t gw = blockIdx.x * kWaves + w;
+    const uint32_t ntiles = (n + 63u) / 64u;
+    const uint32_t nchunk = (ntiles + kC - 1) / kC;
+    u32x4 nx[4];
+    uint16_t nl = 0;
+    auto issue = [&](uint32_t t0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t p = t0 + 16u * k + (lane >> 2);
+            nx[k] = __builtin_nontemporal_load(win + (size_t)min(p, n - 1u) * 4u + (lane & 3u));
+        }
+        nl = len[min(t0 + lane, n - 1u)];
+    };
+    uint32_t first = 0, np = 0;   // buffered chunks: first, first + W, ... (np of them)
+    uint64_t last = kClock ? __builtin_amdgcn_s_memrealtime() / period : 0;
+    auto flush = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t i = 0; i < np; ++i) {
+            const uint32_t base = (first + i * W) * kC * 64u;
+            const uint32_t cnt = min(kC * 64u, n - base);
+            const uint32_t *h = hb[w] + i * kC * 64u;
+            const uint16_t *qq = qb[w] + i * kC * 64u;
+            if (cnt == kC * 64u) {
+                reinterpret_cast<u32x4 *>(hash + base)[lane] = reinterpret_cast<const u32x4 *>(h)[lane];
+                if (lane < 32)
+                    reinterpret_cast<u32x4 *>(q + base)[lane] = reinterpret_cast<const u32x4 *>(qq)[lane];
+            } else {
+                for (uint32_t e = lane; e < cnt; e += 64u) {
+                    hash[base + e] = h[e];
+                    q[base + e] = (int16_t)qq[e];
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        np = 0;
+    };
+    for (uint32_t c = gw; c < nchunk; c += W) {
+        const uint32_t tb = c * kC, te = min(tb + kC, ntiles);
+        if (np == 0)
+            first = c;
+        issue(tb * 64u);
+        for (uint32_t t = tb; t < te; ++t) {
+            u32x4 cur[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                cur[k] = nx[k];
+            const uint16_t cl = nl;
+            if (t + 1 < te)
+                issue((t + 1) * 64u);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                st[w][(16u * k + (lane >> 2)) * 4u + (lane & 3u)] = cur[k];
+            __builtin_amdgcn_wave_barrier();
+            const u32x4 a = st[w][lane * 4u + 0], b = st[w][lane * 4u + 1];
+            const u32x4 cc = st[w][lane * 4u + 2], d = st[w][lane * 4u + 3];
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t x = a.x ^ b.y ^ cc.z ^ d.w ^ cl;
+            hb[w][np * kC * 64u + (t - tb) * 64u + lane] = x;
+            qb[w][np * kC * 64u + (t - tb) * 64u + lane] = (uint16_t)(x & 0x7fffu);
+        }
+        ++np;
+        bool due = np >= cap;
+        if (kClock) {
+            const uint64_t now = __builtin_amdgcn_s_memrealtime() / period;
+            if (now != last) {
+                due = true;
+                last = now;
+            }
+        }
+        if (due)
+            flush();
+    }
+    flush();
+}
+
 }  // namespace
+
+extern "C" int yrss_probe_phase_launch(const void *win, const void *len, void *q, void *hash,
+                                       uint32_t npkts, void *stream, int clock, uint32_t period,
+                                       uint32_t cap)
+{
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return -5;
+    if (npkts == 0)
+        return 0;
+    cap = cap < 1 ? 1 : (cap > kB ? kB : cap);
+    period = period < 1 ? 1 : period;
+    auto k = clock ? yrss_probe_phase<true> : yrss_probe_phase<false>;
+    hipLaunchKernelGGL(k, dim3((unsigned)cus), dim3(512), 0, (hipStream_t)stream,
+                       (const u32x4 *)win, (const uint16_t *)len, (int16_t *)q, (uint32_t *)hash,
+                       npkts, period, cap);
+    return hipGetLastError() == hipSuccess ? 0 : -5;
+}
+
+extern "C" int yrss_probe_traffic_launch_mode(const void *win, const void *len, void *q,
+                                              void *hash, uint32_t npkts, void *stream, int mode);
 
 extern "C" int yrss_probe_traffic_launch(const void *win, const void *len, void *q, void *hash,
                                          uint32_t npkts, void *stream)
+{
+    static int mode = -1;
+    if (mode < 0) {
+        const char *e = getenv("YRSS_PROBE_MODE");
+        mode = e ? atoi(e) : 0;
+    }
+    return yrss_probe_traffic_launch_mode(win, len, q, hash, npkts, stream, mode);
+}
+
+// mode 0: the parse kernel's reads and writes; 1: its reads only; 2: its
+// writes only; 3: see yrss_probe_traffic
+extern "C" int yrss_probe_traffic_launch_mode(const void *win, const void *len, void *q,
+                                              void *hash, uint32_t npkts, void *stream, int mode)
 {
     static int cus = 0;
     if (!cus) {
@@ -115,11 +247,6 @@ extern "C" int yrss_probe_traffic_launch(const void *win, const void *len, void 
     }
     if (npkts == 0)
         return 0;
-    static int mode = -1;
-    if (mode < 0) {
-        const char *e = getenv("YRSS_PROBE_MODE");
-        mode = e ? atoi(e) : 0;
-    }
     auto k = mode == 1   ? yrss_probe_traffic<1>
              : mode == 2 ? yrss_probe_traffic<2>
              : mode == 3 ? yrss_probe_traffic<3>
