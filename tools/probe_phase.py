@@ -53,10 +53,11 @@ def main():
                 stream.cuda_stream)
 
     rows = [("twin (mode 0)", lambda b: mode_fn(*a(b), 0)),
-            ("reads only (mode 1)", lambda b: mode_fn(*a(b), 1))]
-    for cap in (1, 2, 4):
+            ("reads only (mode 1)", lambda b: mode_fn(*a(b), 1)),
+            ("outputs in the window records (mode 5)", lambda b: mode_fn(*a(b), 5))]
+    for cap in (() if "--rows" in sys.argv else (1, 2, 4)):
         rows.append((f"buffer {cap} chunks, no clock", lambda b, cap=cap: ph(*a(b), 0, 1, cap)))
-    for period in (100, 200, 500, 1000):
+    for period in (() if "--rows" in sys.argv else (100, 200, 500, 1000)):
         rows.append((f"buffer 4 chunks, clock period {period * 10} ns",
                      lambda b, p=period: ph(*a(b), 1, p, 4)))
     for rep in range(2):

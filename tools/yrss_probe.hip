@@ -89,6 +89,16 @@ __global__ __launch_bounds__(512) void yrss_probe_traffic(const u32x4 *win, cons
             __builtin_amdgcn_wave_barrier();
             continue;
         }
+        if (kMode == 5) {   // outputs into the packets' own window records (DRAM-row locality test)
+            for (uint32_t j = 0; j < te - tb; ++j) {
+                const uint32_t e = j * 64u + lane;
+                if (base + e < n) {
+                    uint32_t *r = const_cast<uint32_t *>(reinterpret_cast<const uint32_t *>(win + (size_t)(base + e) * 4u));
+                    *reinterpret_cast<uint2 *>(r) = uint2{hb[w][e], (uint32_t)qb[w][e]};
+                }
+            }
+            continue;
+        }
         for (uint32_t j = 0; j < te - tb; ++j) {
             const uint32_t e = j * 64u + lane;
             if (kMode == 1 && hb[w][e] != 0x9e3779b9u)   // reads only: practically never stores
@@ -234,7 +244,8 @@ extern "C" int yrss_probe_traffic_launch(const void *win, const void *len, void 
 }
 
 // mode 0: the parse kernel's reads and writes; 1: its reads only; 2: its
-// writes only; 3: see yrss_probe_traffic
+// writes only; 3: see yrss_probe_traffic; 5: the same writes into the packets'
+// own window records (8 bytes at the start of each), not separate arrays
 extern "C" int yrss_probe_traffic_launch_mode(const void *win, const void *len, void *q,
                                               void *hash, uint32_t npkts, void *stream, int mode)
 {
@@ -250,6 +261,7 @@ extern "C" int yrss_probe_traffic_launch_mode(const void *win, const void *len, 
     auto k = mode == 1   ? yrss_probe_traffic<1>
              : mode == 2 ? yrss_probe_traffic<2>
              : mode == 3 ? yrss_probe_traffic<3>
+             : mode == 5 ? yrss_probe_traffic<5>
                          : yrss_probe_traffic<0>;
     hipLaunchKernelGGL(k, dim3((unsigned)cus), dim3(512), 0, (hipStream_t)stream,
                        (const u32x4 *)win, (const uint16_t *)len, (int16_t *)q, (uint32_t *)hash,
