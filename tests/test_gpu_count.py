@@ -1,6 +1,6 @@
 """Count-mode scatter parity (GPU).
 
-With 10..25 buckets (by default; YRSS_COUNT_MAXNB moves the bound), groups
+With 10..17 buckets (by default; YRSS_COUNT_MAXNB moves the bound), groups
 that feed more than YRSS_COUNT_KMIN buckets (default 8) are ranked by a
 lane-serial counting sort in LDS and leave through the LDS list image
 (yrss.hip scatter_count / image_layout / flush_image); groups feeding fewer
@@ -101,12 +101,12 @@ def test_count_mode_unaligned(oracle_mod, qshift, ishift):
 
 @pytest.mark.parametrize("cfg", [(20, 20, 1, 0), (32, 32, 1, 1), (48, 48, 1, 0)])
 @pytest.mark.parametrize("n", [1025, 4097, 400003])
-@pytest.mark.parametrize("img", [0, 1])
-def test_ranked_image(dev, oracle_mod, cfg, n, img):
+@pytest.mark.parametrize("img,gstage", [(0, 1), (1, 0), (0, 0)])
+def test_ranked_image(dev, oracle_mod, cfg, n, img, gstage):
     """The ranked path (18..65 buckets with count mode held to 17) with its
-    lists built in a packed LDS image (YRSS_RANK_IMG=1; the default up to 33
-    buckets) or through the per-chunk stage (0): the same FIFO lists."""
-    with _env(YRSS_RANK_IMG=img, YRSS_COUNT_MAXNB=17):
+    lists built in one packed stage per group (the default), a packed LDS image
+    (YRSS_RANK_IMG=1) or the per-chunk stage: the same FIFO lists."""
+    with _env(YRSS_RANK_IMG=img, YRSS_RANK_GSTAGE=gstage, YRSS_COUNT_MAXNB=17):
         with SoftRss(*cfg, device=0, max_burst=0) as eng:
             for profile in (abi.SYN_TCP4, abi.SYN_FUZZ):
                 check(eng, oracle_mod, cfg, profile, n, first=n + 3)

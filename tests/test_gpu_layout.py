@@ -153,3 +153,15 @@ def test_scatter_xcd_mapping(dev, oracle_mod, cfg, xcd):
         with SoftRss(*cfg, device=0, max_burst=0) as eng:
             for profile in (abi.SYN_TCP4, abi.SYN_FUZZ):
                 check(eng, oracle_mod, cfg, profile, 777777, first=31)
+
+
+@pytest.mark.parametrize("group", [16, 32, 64])
+@pytest.mark.parametrize("cfg", [(48, 48, 1, 0), (100, 100, 1, 1), (255, 255, 1, 0), (4096, 256, 1, 1)])
+def test_ranked_group_stage(dev, oracle_mod, cfg, group):
+    """YRSS_RANK_GSTAGE: the ranked scatter sorts a whole group in one packed
+    LDS stage (YRSS_RANK_IMG=0 so it also runs at 49 buckets); same lists for
+    any group size, ragged and small batches included."""
+    with _env(YRSS_RANK_GSTAGE=1, YRSS_RANK_IMG=0, YRSS_GROUP_TILES=group):
+        with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            for profile, n in ((abi.SYN_TCP4, 1 << 20), (abi.SYN_FUZZ, 777777), (abi.SYN_IMIX, 5001)):
+                check(eng, oracle_mod, cfg, profile, n, first=47)

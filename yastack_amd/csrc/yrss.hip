@@ -134,6 +134,7 @@ struct ScatterParams {
     uint32_t cnt_off;          // count mode: wave LDS word offset of its counters (0: off)
     uint32_t kmin;             // count mode for groups feeding more than kmin buckets
     uint32_t xcd;              // workgroups of one XCD take consecutive groups (xcd_block)
+    uint32_t gstage;           // ranked stage path: one packed stage per group, not per chunk
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -1426,6 +1427,70 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterPara
         flush_image(P, img, desc, pieces, lane);
         return;
     }
+    if (P.gstage) {
+        // One counting-sort stage for the whole group, entries packed as
+        // (packet - group start) << 9 | bucket: a bucket's run is all its
+        // packets of the group, so each 64-lane store of the copy-out covers
+        // a few long runs instead of one short run per bucket and chunk.
+        // Stage slot = lst[b] + (prefix[b][c] - prefix[b][c0]) + rank.
+        if (c0 >= c1)
+            return;
+        uint32_t *gcur = cur, *coff = lst + P.nb;
+        uint32_t *stg = coff + P.nb;
+        uint32_t ls = 0;
+        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+            const uint32_t b = b0 + lane;
+            uint32_t o = 0, cnt = 0;
+            if (b < P.nb) {
+                const uint32_t *row = P.seg_off + (size_t)b * P.ncol;
+                o = row[c0];
+                cnt = (c1 < P.nchunk ? row[c1] : P.totals[b]) - o;
+            }
+            const uint32_t x = wave_incl_scan(cnt, lane);
+            if (b < P.nb) {
+                gcur[b] = start[b] + o;
+                lst[b] = ls + x - cnt;
+            }
+            ls += __shfl(x, kWave - 1, kWave);
+        }
+        wave_lds_sync();
+        const uint32_t gb = c0 * P.chunk;
+        for (uint32_t c = c0; c < c1; ++c) {
+            for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
+                const uint32_t b = b0 + lane;
+                if (b < P.nb)
+                    coff[b] = lst[b] + P.seg_off[(size_t)b * P.ncol + c] + start[b] - gcur[b];
+            }
+            wave_lds_sync();
+            const uint32_t pb = c * P.chunk;
+            const uint32_t pe = (uint64_t)pb + P.chunk < P.n ? pb + P.chunk : P.n;
+            for (uint32_t p0 = pb; p0 < pe; p0 += kWave * kScatterRound) {
+                int32_t qv[kScatterRound];
+                uint32_t rv[kScatterRound];
+#pragma unroll
+                for (int j = 0; j < kScatterRound; ++j) {
+                    const uint32_t pc = min(p0 + j * kWave + lane, pe - 1u);
+                    qv[j] = P.q[pc];
+                    rv[j] = P.rank[pc];
+                }
+#pragma unroll
+                for (int j = 0; j < kScatterRound; ++j) {
+                    const uint32_t p = p0 + j * kWave + lane;
+                    if (p < pe) {
+                        const uint32_t b = bucket_of((int16_t)qv[j], P.nq);
+                        stg[coff[b] + rv[j]] = ((p - gb) << 9) | b;
+                    }
+                }
+            }
+            wave_lds_sync();
+        }
+        const uint32_t ge = (uint64_t)c1 * P.chunk < P.n ? c1 * P.chunk : P.n;
+        for (uint32_t k = lane; k < ge - gb; k += kWave) {
+            const uint32_t e = stg[k], b = e & 511u;
+            P.qidx[gcur[b] + (k - lst[b])] = gb + (e >> 9);
+        }
+        return;
+    }
     for (uint32_t c = c0; c < c1; ++c) {
         // the chunk's cursor per bucket and its counting-sort layout: bucket b
         // holds stage slots [lst[b], lst[b] + count), count from the prefix
@@ -2283,9 +2348,11 @@ struct yrss_ctx {
     };
     std::vector<Occ> occ;           // resident_blocks cache
     uint32_t count_kmin = kFewBuckets;   // YRSS_COUNT_KMIN: count mode above this many buckets
-    uint32_t count_max_nb = 25;     // YRSS_COUNT_MAXNB: count mode up to this many buckets
+    uint32_t count_max_nb = 17;     // YRSS_COUNT_MAXNB: count mode up to this many buckets
     uint32_t scatter_wpb = 0;       // YRSS_SCATTER_WPB: waves per scatter workgroup (0: auto)
     int scatter_xcd = -1;           // YRSS_SCATTER_XCD: XCD-contiguous scatter groups (-1: auto)
+    bool rank_gstage = true;        // YRSS_RANK_GSTAGE: ranked stage per group, packed entries
+    uint32_t rank_min_nb = 17;      // YRSS_RANK_MINNB: ranked scatter past this many buckets
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
     uint32_t *d_scan_fault = nullptr;   // host-coherent pinned word (yrss_status)
@@ -2455,7 +2522,8 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     // 65 buckets; 4096 for the ranked path at 26..65 buckets
     // (r01_v5_scatter_sweep.log, profiles/r02_v11_count_sweep.log)
     const uint64_t gt = c->group_tiles ? c->group_tiles
-                                       : (c->nb <= c->count_max_nb || c->nb > 65u ? 32u : 64u);
+                                       : (c->nb <= c->count_max_nb || c->nb > 65u || c->rank_gstage
+                                              ? 32u : 64u);
     Layout L;
     L.ct_shift = ct_shift;
     L.shift = 0;
@@ -2479,6 +2547,7 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
 // per bucket (few_img), which also holds a count-mode group's packed runs.
 struct ScatterLds {
     uint32_t aux, img, wlds, wpb, cnt_off, m;
+    uint32_t gstage = 0;   // ranked: one packed stage per group
 };
 constexpr uint32_t kScatterLdsMax = 64u * 1024u / 4u;   // words per workgroup
 
@@ -2506,13 +2575,14 @@ void scatter_wpb(const yrss_ctx *c, ScatterLds &r)
         r.wpb /= 2;
 }
 
-// Count mode: for 10..count_max_nb (25) buckets by default.  With 9 the
+// Count mode: for 10..count_max_nb (17) buckets by default.  With 9 the
 // groups rarely feed more than 8 (nb_procs 8 with dispatch_only_core hashes
 // to 7 queues), and count mode's larger LDS share and unused q loads cost the
-// few-bucket path 8 %; past 25 buckets the ranked path is as fast or faster
-// (runs of a line or two leave the image's whole-line stores little to do:
-// profiles/r02_v11_count_sweep.log).  It needs 32 or 64 packets per lane and
-// its image and counters within one wave's LDS share.
+// few-bucket path 8 %; past 17 buckets the ranked path with its group stage
+// is faster (+5-7 % at 21 buckets: profiles/r02_v26_gstage2_ab.log; before
+// the group stage count mode held up to 25, profiles/r02_v11_count_sweep.log).
+// It needs 32 or 64 packets per lane and its image and counters within one
+// wave's LDS share.
 ScatterLds count_lds(const yrss_ctx *c, const Layout &lay)
 {
     ScatterLds r{};
@@ -2536,11 +2606,15 @@ ScatterLds scatter_lds(const yrss_ctx *c, const Layout &lay, bool ranked)
     const uint32_t nb = c->nb;
     ScatterLds r{};
     if (ranked) {
-        // the packed image and its pieces, else the chunk stage.  The image
-        // gains up to 33 buckets: all-TCP +3 % at 29-33 (the next parse
-        // kernel 10-13 us faster, the scatter 1-4 us slower), IMIX even;
-        // from 37 buckets the scatter's loss is larger than the parse
-        // kernel's gain (profiles/r02_v11_count_sweep.log)
+        // By default one packed counting-sort stage per 2048-packet group
+        // (gstage): all-TCP step against the best earlier path, same box,
+        // +5-7 % at 21 buckets (count mode), +6-7 % at 26-33 (LDS image),
+        // +11-15 % at 41-65 (LDS image), +7.5 % at 129 and +6 % at 256
+        // (per-chunk stage): profiles/r02_v25_gstage_ab.log,
+        // r02_v26_gstage2_ab.log.  With it off: the packed image (its pieces
+        // go out a line part per 8 lanes), which gained up to 33 buckets
+        // (profiles/r02_v11_count_sweep.log; 65 with XCD-contiguous groups),
+        // else the per-chunk stage.
         r.aux = (6u * nb + 3u) & ~3u;
         r.img = lay.seg;
         const uint32_t w = r.aux + r.img + (lay.seg / kImgLine + 2u * nb) * 4u;
@@ -2548,9 +2622,14 @@ ScatterLds scatter_lds(const yrss_ctx *c, const Layout &lay, bool ranked)
         // step +2..6 % at 49, +0.5..2 % at 65; -4 % at 129, -13 % at 256:
         // profiles/r02_v16_rankimg_xcd_ab.log); round-robin, up to 33.
         const uint32_t img_max = scatter_xcd_on(c) ? kRankImgMaxNb : kRankImgMaxNbRr;
-        const bool on = c->rank_img < 0 ? nb <= img_max : c->rank_img > 0;
+        const bool on = c->rank_img < 0 ? !c->rank_gstage && nb <= img_max : c->rank_img > 0;
         if (on && !c->no_img && w <= kScatterLdsMax) {
             r.wlds = w;
+        } else if (c->rank_gstage && lay.seg <= 4096u && nb <= 512u &&
+                   4u * nb + lay.seg <= kScatterLdsMax) {
+            r.aux = r.img = 0;
+            r.gstage = 1;
+            r.wlds = (4u * nb + lay.seg + 3u) & ~3u;
         } else {
             r.aux = r.img = 0;
             r.wlds = 3u * nb + 2u * kRankStage;
@@ -3143,6 +3222,13 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         if (v == 1 || v == 2 || v == 4)
             c->scatter_wpb = (uint32_t)v;
     }
+    if (const char *e = getenv("YRSS_RANK_GSTAGE"))
+        c->rank_gstage = atoi(e) != 0;
+    if (const char *e = getenv("YRSS_RANK_MINNB")) {
+        const int v = atoi(e);
+        if (v >= 2 && v <= YRSS_MAX_QUEUES + 1)
+            c->rank_min_nb = (uint32_t)v;
+    }
     if (const char *e = getenv("YRSS_SCATTER_XCD"))
         c->scatter_xcd = atoi(e) != 0 ? 1 : 0;
     if (const char *e = getenv("YRSS_GROUP_TILES")) {
@@ -3365,16 +3451,17 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     }
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
-    // Past 17 buckets with 16-tile chunks, when count mode does not take the
-    // batch (26..256 buckets by default): the parse kernel also emits each
-    // packet's rank in its chunk and the scatter places it by that rank.
+    // Past 17 buckets (YRSS_RANK_MINNB) with 16-tile chunks, when count mode
+    // does not take the batch (18..256 buckets by default): the parse kernel
+    // also emits each packet's rank in its chunk and the scatter places it by
+    // that rank.
     // Measured against the ballot scatter: step -4 % at 33 buckets, -2 % at
     // 17, +3 % at 65, +9 % at 129, even at 256; at 10 buckets (256-packet
     // chunks) the ranks' cost in the parse kernel (+5-8 us) outweighed the
     // gain, and chunks above kRankStage packets do not fit the stage.
     const ScatterLds cl = compact ? count_lds(c, lay) : ScatterLds{};
     const bool ranked =
-        compact && !c->no_rank && !cl.cnt_off && c->nb > 17u && lay.chunk <= kRankStage;
+        compact && !c->no_rank && !cl.cnt_off && c->nb > c->rank_min_nb && lay.chunk <= kRankStage;
     if (ranked && c->rank_cap < n) {
         if (c->d_rank) {
             YRSS_HIP(hipStreamSynchronize(s));
@@ -3455,6 +3542,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.cnt_off = sl.cnt_off;
     S.kmin = c->count_kmin;
     S.xcd = scatter_xcd_on(c) ? 1u : 0u;
+    S.gstage = ranked ? sl.gstage : 0u;
     {
         void (*fn)(ScatterParams) = ranked          ? yrss_scatter_ranked
                                     : sl.m == 64u ? yrss_scatter<64>
