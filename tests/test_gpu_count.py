@@ -1,6 +1,6 @@
 """Count-mode scatter parity (GPU).
 
-With 10..17 buckets (by default; YRSS_COUNT_MAXNB moves the bound), groups
+With 10..YRSS_COUNT_MAXNB buckets (off by default since the ranked group stage), groups
 that feed more than YRSS_COUNT_KMIN buckets (default 8) are ranked by a
 lane-serial counting sort in LDS and leave through the LDS list image
 (yrss.hip scatter_count / image_layout / flush_image); groups feeding fewer
@@ -49,7 +49,7 @@ def test_count_mode_threshold(dev, oracle_mod, kmin, profile):
     """A low threshold sends groups with few buckets (IMIX / UDP stretches)
     through count mode too, mixed with few-bucket groups in one launch."""
     cfg = (12, 12, 1, 1)
-    with _env(YRSS_COUNT_KMIN=kmin):
+    with _env(YRSS_COUNT_KMIN=kmin, YRSS_COUNT_MAXNB=ANY_NB):
         with SoftRss(*cfg, device=0, max_burst=0) as eng:
             check(eng, oracle_mod, cfg, profile, 262144 + 4097, first=5)
 
@@ -73,12 +73,14 @@ def test_count_mode_matches_ballot_path(dev, oracle_mod):
                 check(eng, oracle_mod, cfg, abi.SYN_TCP4, 1 << 21, first=8)
 
 
+@pytest.mark.parametrize("count_maxnb", [ANY_NB, 9])
 @pytest.mark.parametrize("qshift,ishift", [(1, 1), (3, 2), (5, 3)])
-def test_count_mode_unaligned(oracle_mod, qshift, ishift):
+def test_count_mode_unaligned(oracle_mod, qshift, ishift, count_maxnb):
     """q at 2-byte alignment (count mode loads it as 16-byte vectors) and qidx
-    at 4-byte alignment, n odd; nothing written outside qidx."""
+    at 4-byte alignment, n odd; nothing written outside qidx.  Count mode, and
+    the default ranked group stage at the same bucket count."""
     n, stride, cfg = 300007, 64, (16, 16, 1, 0)
-    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+    with _env(YRSS_COUNT_MAXNB=count_maxnb), SoftRss(*cfg, device=0, max_burst=0) as eng:
         win, lens = eng.synth(abi.SYN_TCP4, n, 3, stride=stride)
         d = win.device
         qi_buf = torch.full((n + 8,), -1, dtype=torch.int32, device=d)

@@ -28,11 +28,11 @@ CONFIGS = [
 # the same all-hashed stream over more dispatch queues (nb_procs lcores,
 # dispatch_only_core): each scatter path in turn (yrss.hip)
 QUEUES = [
-    ("q8", "tcp4", "64B TCP/IPv4, nb_procs 8 (9 buckets: few-bucket path)", ["--nb-procs", "8"]),
-    ("q16", "tcp4", "64B TCP/IPv4, nb_procs 16 (17 buckets: count mode, XCD-contiguous groups)", ["--nb-procs", "16"]),
-    ("q32", "tcp4", "64B TCP/IPv4, nb_procs 32 (33 buckets: ranked, LDS image, XCD-contiguous groups)", ["--nb-procs", "32"]),
-    ("q64", "tcp4", "64B TCP/IPv4, nb_procs 64 (65 buckets: ranked, LDS image, XCD-contiguous groups)", ["--nb-procs", "64"]),
-    ("q255", "tcp4", "64B TCP/IPv4, nb_procs 255 (256 buckets: ranked, XCD-contiguous groups)", ["--nb-procs", "255"]),
+    ("q8", "tcp4", "64B TCP/IPv4, nb_procs 8 (9 buckets: ranked, group stage)", ["--nb-procs", "8"]),
+    ("q16", "tcp4", "64B TCP/IPv4, nb_procs 16 (17 buckets: ranked, group stage, XCD-contiguous groups)", ["--nb-procs", "16"]),
+    ("q32", "tcp4", "64B TCP/IPv4, nb_procs 32 (33 buckets: ranked, group stage, XCD-contiguous groups)", ["--nb-procs", "32"]),
+    ("q64", "tcp4", "64B TCP/IPv4, nb_procs 64 (65 buckets: ranked, group stage, XCD-contiguous groups)", ["--nb-procs", "64"]),
+    ("q255", "tcp4", "64B TCP/IPv4, nb_procs 255 (256 buckets: ranked, group stage, XCD-contiguous groups)", ["--nb-procs", "255"]),
 ]
 
 

@@ -2348,11 +2348,11 @@ struct yrss_ctx {
     };
     std::vector<Occ> occ;           // resident_blocks cache
     uint32_t count_kmin = kFewBuckets;   // YRSS_COUNT_KMIN: count mode above this many buckets
-    uint32_t count_max_nb = 17;     // YRSS_COUNT_MAXNB: count mode up to this many buckets
+    uint32_t count_max_nb = 9;      // YRSS_COUNT_MAXNB: count mode up to this many buckets (off)
     uint32_t scatter_wpb = 0;       // YRSS_SCATTER_WPB: waves per scatter workgroup (0: auto)
     int scatter_xcd = -1;           // YRSS_SCATTER_XCD: XCD-contiguous scatter groups (-1: auto)
     bool rank_gstage = true;        // YRSS_RANK_GSTAGE: ranked stage per group, packed entries
-    uint32_t rank_min_nb = 17;      // YRSS_RANK_MINNB: ranked scatter past this many buckets
+    uint32_t rank_min_nb = 8;       // YRSS_RANK_MINNB: ranked scatter past this many buckets
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
     uint32_t *d_scan_fault = nullptr;   // host-coherent pinned word (yrss_status)
@@ -2575,14 +2575,15 @@ void scatter_wpb(const yrss_ctx *c, ScatterLds &r)
         r.wpb /= 2;
 }
 
-// Count mode: for 10..count_max_nb (17) buckets by default.  With 9 the
-// groups rarely feed more than 8 (nb_procs 8 with dispatch_only_core hashes
-// to 7 queues), and count mode's larger LDS share and unused q loads cost the
-// few-bucket path 8 %; past 17 buckets the ranked path with its group stage
-// is faster (+5-7 % at 21 buckets: profiles/r02_v26_gstage2_ab.log; before
-// the group stage count mode held up to 25, profiles/r02_v11_count_sweep.log).
-// It needs 32 or 64 packets per lane and its image and counters within one
-// wave's LDS share.
+// Count mode: for 10..count_max_nb buckets, off by default since the ranked
+// path's group stage: that was +5-7 % at 21 buckets
+// (profiles/r02_v26_gstage2_ab.log) and +0.5-3 % at 13 and 17
+// (profiles/r02_v27_gstage3_ab.log); before it count mode held 10..25
+// (profiles/r02_v11_count_sweep.log).  With 9 buckets the groups rarely feed
+// more than 8 (nb_procs 8 with dispatch_only_core hashes to 7 queues), and
+// count mode's larger LDS share and unused q loads cost the few-bucket path
+// 8 %.  It needs 32 or 64 packets per lane and its image and counters within
+// one wave's LDS share.
 ScatterLds count_lds(const yrss_ctx *c, const Layout &lay)
 {
     ScatterLds r{};
@@ -3451,10 +3452,11 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     }
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
-    // Past 17 buckets (YRSS_RANK_MINNB) with 16-tile chunks, when count mode
-    // does not take the batch (18..256 buckets by default): the parse kernel
-    // also emits each packet's rank in its chunk and the scatter places it by
-    // that rank.
+    // Past 8 buckets (YRSS_RANK_MINNB), when count mode does not take the
+    // batch (9..256 buckets by default): the parse kernel also emits each
+    // packet's rank in its chunk and the scatter places it by that rank
+    // (group stage: +2-7 % at 9 buckets over the few-bucket path,
+    // profiles/r02_v27_gstage3_ab.log).
     // Measured against the ballot scatter: step -4 % at 33 buckets, -2 % at
     // 17, +3 % at 65, +9 % at 129, even at 256; at 10 buckets (256-packet
     // chunks) the ranks' cost in the parse kernel (+5-8 us) outweighed the
