@@ -156,7 +156,7 @@ def test_scatter_xcd_mapping(dev, oracle_mod, cfg, xcd):
 
 
 @pytest.mark.parametrize("group", [16, 32, 64])
-@pytest.mark.parametrize("cfg", [(8, 8, 1, 0), (12, 12, 1, 1), (16, 16, 1, 0), (48, 48, 1, 0),
+@pytest.mark.parametrize("cfg", [(7, 7, 1, 0), (8, 8, 1, 0), (12, 12, 1, 1), (16, 16, 1, 0), (48, 48, 1, 0),
                                  (100, 100, 1, 1), (255, 255, 1, 0), (4096, 256, 1, 1)])
 def test_ranked_group_stage(dev, oracle_mod, cfg, group):
     """YRSS_RANK_GSTAGE: the ranked scatter sorts a whole group in one packed

@@ -2352,7 +2352,7 @@ struct yrss_ctx {
     uint32_t scatter_wpb = 0;       // YRSS_SCATTER_WPB: waves per scatter workgroup (0: auto)
     int scatter_xcd = -1;           // YRSS_SCATTER_XCD: XCD-contiguous scatter groups (-1: auto)
     bool rank_gstage = true;        // YRSS_RANK_GSTAGE: ranked stage per group, packed entries
-    uint32_t rank_min_nb = 8;       // YRSS_RANK_MINNB: ranked scatter past this many buckets
+    uint32_t rank_min_nb = 7;       // YRSS_RANK_MINNB: ranked scatter past this many buckets
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
     uint32_t *d_scan_fault = nullptr;   // host-coherent pinned word (yrss_status)
@@ -3452,11 +3452,12 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     }
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
-    // Past 8 buckets (YRSS_RANK_MINNB), when count mode does not take the
-    // batch (9..256 buckets by default): the parse kernel also emits each
+    // Past 7 buckets (YRSS_RANK_MINNB), when count mode does not take the
+    // batch (8..256 buckets by default): the parse kernel also emits each
     // packet's rank in its chunk and the scatter places it by that rank
-    // (group stage: +2-7 % at 9 buckets over the few-bucket path,
-    // profiles/r02_v27_gstage3_ab.log).
+    // (group stage over the few-bucket path: +0.7-1 % at 8 buckets, +2-7 % at
+    // 9, -3 % at 6 and -5 % at 4: profiles/r02_v27_gstage3_ab.log,
+    // r02_v28_rankmin_ab.log).
     // Measured against the ballot scatter: step -4 % at 33 buckets, -2 % at
     // 17, +3 % at 65, +9 % at 129, even at 256; at 10 buckets (256-packet
     // chunks) the ranks' cost in the parse kernel (+5-8 us) outweighed the
