@@ -280,6 +280,10 @@ __device__ __forceinline__ uint32_t tz_valu(uint32_t w, const uint32_t *kw, uint
     return h;
 }
 
+#ifndef YRSS_CNT_WG
+#define YRSS_CNT_WG 1   // parse count slots flushed by the workgroup, 8 columns per row
+#endif
+
 #ifndef YRSS_VALU_WORDS
 #define YRSS_VALU_WORDS 0
 #endif
@@ -667,8 +671,26 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
                 break;
         }
     }
-    const uint32_t k = P.nchunk > gw ? (P.nchunk - gw + W - 1) / W : 0u;   // chunks owned
-    if (kCount) {
+    if (kCount && YRSS_CNT_WG) {
+        // Workgroup flush: for its j-th chunk each of the 8 waves owns column
+        // blockIdx.x * 8 + w + j * W, so the workgroup's columns of round j
+        // are 8 consecutive words of every bucket row.  Thread e takes wave
+        // e % 8, bucket (e / 8) % nb, round e / (8 nb): a 64-lane store then
+        // covers 8 rows x 32 contiguous bytes instead of one word in each of
+        // 64 rows (a store costs the lines its lanes touch).
+        __syncthreads();
+        const uint32_t g0 = blockIdx.x * kWaves;
+        const uint32_t kmax = P.nchunk > g0 ? (P.nchunk - g0 + W - 1) / W : 0u;
+        const uint32_t per_round = kWaves * P.nb;
+        for (uint32_t e = threadIdx.x; e < kmax * per_round; e += kBlock) {
+            const uint32_t j = e / per_round, r = e - j * per_round;
+            const uint32_t b = r / kWaves, w = r - b * kWaves;
+            const uint32_t col = g0 + w + j * W;
+            if (col < P.nchunk)
+                P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
+        }
+    } else if (kCount) {
+        const uint32_t k = P.nchunk > gw ? (P.nchunk - gw + W - 1) / W : 0u;   // chunks owned
         wave_lds_sync();
         for (uint32_t j = 0; j < k; ++j)
             for (uint32_t b = lane; b < P.nb; b += kWave)
