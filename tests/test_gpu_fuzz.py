@@ -4,6 +4,7 @@ and starting packet drawn at random (40 cases, each small enough for the
 oracle).  And two host threads driving their own contexts at once (the GIL is
 released inside every ctypes call), each checked against the oracle.
 """
+import os
 import threading
 
 import numpy as np
@@ -42,7 +43,9 @@ def _cases(count, seed):
     return out
 
 
-@pytest.mark.parametrize("case", _cases(40, 2024))
+# YRSS_FUZZ_CASES / YRSS_FUZZ_SEED widen the sweep for a soak run
+@pytest.mark.parametrize("case", _cases(int(os.environ.get("YRSS_FUZZ_CASES", "40")),
+                                        int(os.environ.get("YRSS_FUZZ_SEED", "2024"))))
 def test_random_configs(dev, oracle_mod, case):
     npr, nq, soft, only, stride, profile, n, first = case
     with SoftRss(npr, nq, soft, only, device=0, max_burst=0) as eng:
