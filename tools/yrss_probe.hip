@@ -7,8 +7,9 @@
 //   - each tile's four 16-byte non-temporal loads in flight while the previous
 //     tile is handled (one tile ahead);
 //   - the window reaches its packet's lane through LDS;
-//   - outputs buffered in LDS and written per chunk as one burst of plain
-//     stores.
+//   - outputs buffered in LDS and written per chunk as one burst of 16-byte
+//     stores (1 KiB of hash, 512 B of q per wave-instruction), the parse
+//     kernel's form; loads run one tile ahead across chunk boundaries too.
 // Its duration on a given box is the practical floor for the parse kernel's
 // traffic there; bench.py reports the parse kernel against it next to the
 // 8 TB/s spec peak, so box-to-box HBM variance is visible.
@@ -56,17 +57,29 @@ __global__ __launch_bounds__(512) void yrss_probe_traffic(const u32x4 *win, cons
         }
         nl = len[min(t0 + lane, n - 1u)];
     };
+    // the wave's tiles form one sequence across its chunks (as in the parse
+    // kernel), loaded one tile ahead across chunk boundaries too
+    auto tile_of = [&](uint32_t i) -> uint32_t {   // ntiles when past the wave's last
+        const uint32_t c = gw + (i / kC) * W;
+        if (c >= nchunk)
+            return ntiles;
+        const uint32_t t = c * kC + i % kC;
+        return t < ntiles ? t : ntiles;
+    };
+    uint32_t seq = 0;
+    if (tile_of(0) < ntiles)
+        issue(tile_of(0) * 64u);
     for (uint32_t c = gw; c < nchunk; c += W) {
         const uint32_t tb = c * kC, te = min(tb + kC, ntiles);
-        issue(tb * 64u);
-        for (uint32_t t = tb; t < te; ++t) {
+        for (uint32_t t = tb; t < te; ++t, ++seq) {
             u32x4 cur[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 cur[k] = nx[k];
             const uint16_t cl = nl;
-            if (t + 1 < te)
-                issue((t + 1) * 64u);
+            const uint32_t tn = tile_of(seq + 1);
+            if (tn < ntiles)
+                issue(tn * 64u);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 st[w][(16u * k + (lane >> 2)) * 4u + (lane & 3u)] = cur[k];
@@ -79,13 +92,18 @@ __global__ __launch_bounds__(512) void yrss_probe_traffic(const u32x4 *win, cons
             qb[w][(t - tb) * 64u + lane] = (uint16_t)(x & 0x7fffu);
         }
         const uint32_t base = tb * 64u;
-        if (kMode == 3 && te - tb == kC) {   // writes only, 16 bytes per lane per store
+        if ((kMode == 3 || kMode == 0) && te - tb == kC) {   // 16 bytes per lane per store, as the parse kernel's bursts
             __builtin_amdgcn_wave_barrier();
-            reinterpret_cast<u32x4 *>(hash + base)[lane] =
-                reinterpret_cast<const u32x4 *>(hb[w])[lane];
+            // write-through (sc1) 16-byte stores, exactly the parse kernel's burst form
+            const __amdgpu_buffer_rsrc_t rh =
+                __builtin_amdgcn_make_buffer_rsrc(hash + base, 0, (int)(kC * 64u * 4u), 0x00020000);
+            const __amdgpu_buffer_rsrc_t rq =
+                __builtin_amdgcn_make_buffer_rsrc(q + base, 0, (int)(kC * 64u * 2u), 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(reinterpret_cast<const u32x4 *>(hb[w])[lane], rh,
+                                                   (int)(lane * 16u), 0, 16);
             if (lane < 32)
-                reinterpret_cast<u32x4 *>(q + base)[lane] =
-                    reinterpret_cast<const u32x4 *>(qb[w])[lane];
+                __builtin_amdgcn_raw_buffer_store_b128(reinterpret_cast<const u32x4 *>(qb[w])[lane], rq,
+                                                       (int)(lane * 16u), 0, 16);
             __builtin_amdgcn_wave_barrier();
             continue;
         }
