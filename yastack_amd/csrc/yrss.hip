@@ -1500,7 +1500,9 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterPara
                     const uint32_t p = p0 + j * kWave + lane;
                     if (p < pe) {
                         const uint32_t b = bucket_of((int16_t)qv[j], P.nq);
-                        stg[coff[b] + rv[j]] = ((p - gb) << 9) | b;
+                        const uint32_t slot = coff[b] + rv[j];
+                        if (slot < P.seg)   // guard: counts and ranks always agree
+                            stg[slot] = ((p - gb) << 9) | b;
                     }
                 }
             }
@@ -1509,7 +1511,9 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterPara
         const uint32_t ge = (uint64_t)c1 * P.chunk < P.n ? c1 * P.chunk : P.n;
         for (uint32_t k = lane; k < ge - gb; k += kWave) {
             const uint32_t e = stg[k], b = e & 511u;
-            P.qidx[gcur[b] + (k - lst[b])] = gb + (e >> 9);
+            const uint32_t d = b < P.nb ? gcur[b] + (k - lst[b]) : P.n;
+            if (d < P.n)   // guard: a stage slot left unwritten never faults
+                P.qidx[d] = gb + (e >> 9);
         }
         return;
     }
