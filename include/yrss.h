@@ -503,8 +503,9 @@ int yrss_fanout_route(uint64_t ticket, uint32_t nctx, uint32_t *ctx, uint64_t *c
 
 /* Synchronises the device and reports (then clears) a device-side fault of an
  * earlier yrss_dispatch_dev*: 0 = none, -EIO = the per-queue scan's look-back did not
- * resolve, so that batch's qidx/qstart are invalid (q and hash are not
- * affected).  The host-synchronous entry points check this themselves and
+ * resolve, or the ranked scatter found a slot outside its group's lists (it
+ * then stores nothing there), so that batch's qidx/qstart are invalid (q and
+ * hash are not affected).  The host-synchronous entry points check this themselves and
  * return -EIO.  The reference has no equivalent: its per-packet
  * rte_ring_enqueue cannot fail this way (ff_dpdk_if.c:1087-1093). */
 int yrss_status(yrss_ctx *ctx);

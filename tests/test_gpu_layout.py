@@ -34,6 +34,7 @@ def check(eng, oracle_mod, cfg_tuple, profile, n, stride=64, first=0):
     win, lens = eng.synth(profile, n, first, stride=stride)
     res = eng.dispatch_dev(win, lens, stride, n)
     torch.cuda.synchronize()
+    assert eng.status() == 0   # no scan look-back or scatter guard fired
     w_h = win[: n * stride].cpu().numpy()
     l_h = to_np(lens[:n], np.uint16)
     c = oracle_mod.cfg(npr, nq, soft, only)

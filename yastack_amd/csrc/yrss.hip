@@ -135,6 +135,7 @@ struct ScatterParams {
     uint32_t kmin;             // count mode for groups feeding more than kmin buckets
     uint32_t xcd;              // workgroups of one XCD take consecutive groups (xcd_block)
     uint32_t gstage;           // ranked stage path: one packed stage per group, not per chunk
+    uint32_t *fault;           // host-coherent fault word (the scan's): a guard that fired
 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
@@ -1503,6 +1504,9 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterPara
                         const uint32_t slot = coff[b] + rv[j];
                         if (slot < P.seg)   // guard: counts and ranks always agree
                             stg[slot] = ((p - gb) << 9) | b;
+                        else if (P.fault)   // reported as -EIO (yrss_status), never a fault
+                            __hip_atomic_store(P.fault, 2u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                 }
             }
@@ -1514,6 +1518,8 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterPara
             const uint32_t d = b < P.nb ? gcur[b] + (k - lst[b]) : P.n;
             if (d < P.n)   // guard: a stage slot left unwritten never faults
                 P.qidx[d] = gb + (e >> 9);
+            else if (P.fault)
+                __hip_atomic_store(P.fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         return;
     }
@@ -3572,6 +3578,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.kmin = c->count_kmin;
     S.xcd = scatter_xcd_on(c) ? 1u : 0u;
     S.gstage = ranked ? sl.gstage : 0u;
+    S.fault = c->d_scan_fault;
     {
         void (*fn)(ScatterParams) = ranked          ? yrss_scatter_ranked
                                     : sl.m == 64u ? yrss_scatter<64>

@@ -411,7 +411,8 @@ class SoftRss:
 
     def status(self) -> int:
         """Synchronise and return (then clear) the device-side fault state:
-        0, or -EIO if the scan's look-back did not resolve (yrss_status)."""
+        0, or -EIO if the scan's look-back did not resolve or the ranked
+        scatter's index guard fired (yrss_status)."""
         return int(self._lib.yrss_status(self._ctx))
 
     def grid_for(self, n: int) -> int:
