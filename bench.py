@@ -255,19 +255,22 @@ def cpu_baseline(args, nb_queues):
     Both ports (bit-serial as the reference writes toeplitz_hash, and
     table-driven), on the headline UDP stream and all-TCP, on 1 core (the
     reference's single dispatching lcore, ff_dpdk_if.c:1653) and on every core
-    this job may use (at most 16: one GPU's share of the box), as independent
-    processes pinned one per core.  `value` is the bit-serial port on 1 core
-    over the bench's own stream (measured first, then udp4 and tcp4)."""
+    one GPU's share of the box (16), as independent
+    processes pinned one per core, and on every core the process may use
+    (sched_getaffinity: nproc on a dedicated box), SURVEY §8(d).  `value` is
+    the bit-serial port on 1 core over the bench's own stream (measured first,
+    then udp4 and tcp4)."""
     cpus = sorted(os.sched_getaffinity(0))
-    cpus_all = cpus[: max(1, min(16, len(cpus)))]
+    share = cpus[: max(1, min(16, len(cpus)))]      # one GPU's share of the box's cores
+    cells = [cpus[:1], share] + ([cpus] if len(cpus) > len(share) else [])
     profs = list(dict.fromkeys([args.profile, *CPU_PROFILES]))   # the bench's own stream first
-    secs = max(0.5, args.cpu_seconds / (2 * len(profs) * len(CPU_VARIANTS)))
+    secs = max(0.5, args.cpu_seconds / (len(cells) * len(profs) * len(CPU_VARIANTS)))
     by = {}
     for prof in profs:
         by[prof] = {}
         for var in CPU_VARIANTS:
-            by[prof][var] = {"1": round(_cpu_run(prof, var, secs, cpus_all[:1]), 2),
-                             str(len(cpus_all)): round(_cpu_run(prof, var, secs, cpus_all), 2)}
+            by[prof][var] = {str(len(cs)): round(_cpu_run(prof, var, secs, cs), 2)
+                             for cs in cells}
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -282,8 +285,13 @@ def cpu_baseline(args, nb_queues):
         "sample": f"2^20 packets of each stream re-run for ~{secs:.1f}s per cell, one "
                   "toeplitz_dispatch call per packet (oracle restatement, gcc -O2 fs/lib "
                   f"flags), processes pinned one per core; host CPU: {cpu}",
-        "all_cores": {"value": by[head]["bit_serial"][str(len(cpus_all))], "unit": "Mpkt/s",
-                      "cores": len(cpus_all)},
+        "per_gpu_share": {"value": by[head]["bit_serial"][str(len(share))], "unit": "Mpkt/s",
+                          "cores": len(share),
+                          "note": "the 16 host cores one GPU of the box is given"},
+        "all_cores": {"value": by[head]["bit_serial"][str(len(cpus))], "unit": "Mpkt/s",
+                      "cores": len(cpus),
+                      "note": "every core this process may run on (sched_getaffinity), "
+                              "one pinned process per core"},
         "by_profile": by,
     }
 
@@ -418,6 +426,29 @@ def load_traffic(path: str, key: dict, field: str = "hbm_bytes_per_launch"):
     return None
 
 
+def min_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([x], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
+def reduce_check(mine, world: int):
+    """Every rank checks its own shard after timing; the printed line is the
+    AND over ranks (one failing shard makes bit_exact false) with each rank's
+    own result beside it."""
+    if mine is None:
+        return None
+    ok = min_over_ranks(1.0 if mine["bit_exact"] else 0.0, world) > 0.5
+    ranks = gather_objects(mine, world)
+    return {"pkts_checked": sum(r["pkts_checked"] for r in ranks), "bit_exact": ok,
+            "ranks_checked": len(ranks), "per_rank": ranks if world > 1 else None}
+
+
 def check_devices(ident: str, world: int):
     """Every rank's device; N ranks must drive N distinct GPUs (except the
     declared one-device rehearsal, YRSS_BENCH_ONE_DEVICE)."""
@@ -440,11 +471,22 @@ def dry_run(args, world, rank, local):
     barrier(world)
     elapsed = max_over_ranks(t1 - t0, world)
     total = sum_over_ranks(float(args.pkts * args.steps), world)
+    # the check's plumbing: each rank compares its shard's oracle answer with
+    # itself (no device), YRSS_BENCH_DRY_FAIL_RANK marks one rank's shard bad
+    mine = None
+    if args.check:
+        mine = {"rank": rank, "device": devices[rank], "pkts_checked": min(args.check, args.pkts),
+                "bit_exact": os.environ.get("YRSS_BENCH_DRY_FAIL_RANK") != str(rank)}
+    check = reduce_check(mine, world)
+    cpu = cpu_baseline(args, args.nb_queues or args.nb_procs) \
+        if rank == 0 and args.cpu_seconds > 0 else None
+    barrier(world)
     if rank == 0:
         print(json.dumps({"metric": "dry run (no GPU work)", "dry": True, "value": None,
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "pkts_total": total, "elapsed_s": elapsed,
-                          "config": {"parallelism": f"shard{world}", "devices": devices}}),
+                          "config": {"parallelism": f"shard{world}", "devices": devices},
+                          "cpu_baseline": cpu, "check": check}),
               flush=True)
     if world > 1:
         import torch.distributed as dist
@@ -574,11 +616,17 @@ def main(argv=None):
             qi_ref, qs_ref = oracle.process_burst(q_all, nbq)
             ok = ok and bool(np.array_equal(out.qstart.cpu().numpy().view(np.uint32), qs_ref) and
                              np.array_equal(out.qidx[:n].cpu().numpy().view(np.uint32), qi_ref))
-        check = {"pkts_checked": m, "bit_exact": ok}
+        check = {"rank": rank, "device": devices[rank], "pkts_checked": m, "bit_exact": ok,
+                 "parse_us": round(k_ms / max(k_cnt, 1) * 1e3, 2)}
+    check = reduce_check(check, world)
 
+    # the CPU baseline on rank 0 once every rank's device work is done (at any
+    # N: the other ranks wait at the barrier)
+    barrier(world)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, nbq)
+    barrier(world)
     pcie = fan = None
     if args.pcie:
         barrier(world)                    # every rank's device work is done

@@ -147,7 +147,7 @@ void yrss_fini(yrss_ctx *ctx);
  * n <= YRSS_MAX_BATCH.  Asynchronous: returns after enqueueing the kernels.
  * Batches of <= 4096 packets (with nb_queues + 1 <= 64) run as one launch of
  * the one-workgroup burst kernel instead of parse + scan + scatter (same
- * outputs; yrss_timing_* does not count it; YRSS_SMALL_DEV=0 turns it off).
+ * outputs; yrss_timing_* does not count it; yrss_tuning.one_launch turns it off).
  * Dispatches of one context share its compaction workspace: a dispatch on a
  * different stream than the context's previous one waits (on the device) for
  * the work already queued there, so streams may be mixed freely; dispatches
@@ -415,6 +415,9 @@ int yrss_synth_dev(yrss_ctx *ctx, const struct yrss_synth_params *p,
 #define YRSS_K_SCAN       1
 #define YRSS_K_SCATTER    2
 #define YRSS_K_COUNT      3
+/* Kernel ids that appear only in fault records (not timed). */
+#define YRSS_K_BURST      8   /* yrss_burst_small: one-launch bursts / batches */
+#define YRSS_K_WORKER     9   /* yrss_burst_worker */
 int yrss_timing_enable(yrss_ctx *ctx, int kernel_mask);
 int yrss_timing_read(yrss_ctx *ctx, int kernel, double *total_ms,
                      uint32_t *launches);
@@ -501,14 +504,47 @@ int yrss_fanout_route(uint64_t ticket, uint32_t nctx, uint32_t *ctx, uint64_t *c
 
 /* ---- device-side status ----------------------------------------------------------- */
 
-/* Synchronises the device and reports (then clears) a device-side fault of an
- * earlier yrss_dispatch_dev*: 0 = none, -EIO = the per-queue scan's look-back did not
- * resolve, or the ranked scatter found a slot outside its group's lists (it
- * then stores nothing there), so that batch's qidx/qstart are invalid (q and
- * hash are not affected).  The host-synchronous entry points check this themselves and
- * return -EIO.  The reference has no equivalent: its per-packet
- * rte_ring_enqueue cannot fail this way (ff_dpdk_if.c:1087-1093). */
+/* Every index the per-queue lists are built from (count slots, stage slots,
+ * list slots) is bounds-checked on the GPU.  A check that fails stores nothing
+ * and sets the context's fault record (first fault wins): that batch's
+ * qidx/qstart are invalid; q and hash are not affected.  Codes: */
+#define YRSS_FAULT_NONE           0
+#define YRSS_FAULT_SCAN_TIMEOUT   1   /* scan look-back did not resolve: where = bucket row  */
+#define YRSS_FAULT_LIST_RANGE     2   /* list slot >= n: where = packet, value = slot        */
+#define YRSS_FAULT_COUNT_MISMATCH 3   /* a span's histogram differs from the parse counts:
+                                         where = span, value = bucket                        */
+#define YRSS_FAULT_COUNT_SLOT     4   /* parse count slot beyond LDS: where = wave, value = slot */
+#define YRSS_FAULT_STAGE          5   /* scatter stage slot out of range: where = packet     */
+struct yrss_fault {
+    uint32_t code;     /* YRSS_FAULT_*                                   */
+    uint32_t kernel;   /* YRSS_K_* of the kernel whose guard fired       */
+    uint32_t where;
+    uint32_t value;
+};
+
+/* Synchronises the device and reports (then clears) the fault record: 0 = no
+ * guard fired since the last call, -EIO = one did (the record is printed to
+ * stderr).  The host-synchronous entry points check it themselves and return
+ * -EIO, as does yrss_worker_poll.  The reference has no equivalent: its
+ * per-packet rte_ring_enqueue cannot fail this way (ff_dpdk_if.c:1087-1093). */
 int yrss_status(yrss_ctx *ctx);
+/* Same, copying the record (code 0 = none) instead of printing it. */
+int yrss_fault_info(yrss_ctx *ctx, struct yrss_fault *out);
+
+/* ---- layout overrides (tests and measurements) ------------------------------------ */
+
+/* Every field 0 (scatter_xcd -1) is the built-in default; results never
+ * depend on these, only the work layout does. */
+struct yrss_tuning {
+    uint32_t chunk_tiles;    /* parse chunk in 64-packet tiles, power of two (default 4,
+                                larger when a wave's count slots run out)            */
+    uint32_t span_tiles;     /* scatter span in tiles, power of two (default 32)     */
+    uint32_t parse_blocks;   /* parse grid (default one workgroup per CU)            */
+    uint32_t one_launch;     /* batches <= 4096 packets in one launch: 0 host bursts
+                                and device batches, 1 host bursts only, 2 never      */
+    int32_t  scatter_xcd;    /* XCD-contiguous scatter spans: -1 default (on), 0, 1  */
+};
+int yrss_set_tuning(yrss_ctx *ctx, const struct yrss_tuning *t);
 
 /* ---- introspection --------------------------------------------------------------- */
 

@@ -24,3 +24,18 @@ def oracle_mod():
 @pytest.fixture(scope="session")
 def golden_dir():
     return ROOT / "tests" / "golden"
+
+
+@pytest.fixture(autouse=True)
+def _no_device_fault():
+    """Every GPU test: no list guard may fire in any context it closes
+    (yastack_amd.abi.FAULT_LOG, filled by SoftRss.close from the context's
+    fault record), whether or not the test reads yrss_status itself."""
+    try:
+        from yastack_amd import abi
+    except Exception:   # pragma: no cover - import errors surface in the test itself
+        yield
+        return
+    abi.FAULT_LOG.clear()
+    yield
+    assert not abi.FAULT_LOG, f"device guard fired: {abi.FAULT_LOG}"

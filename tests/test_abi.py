@@ -4,6 +4,7 @@ fail them, and the Python constants agree with the header."""
 import ctypes
 import errno
 import re
+import os
 import subprocess
 
 import pytest
@@ -104,3 +105,21 @@ def test_toeplitz_dispatch_without_context_is_an_error():
     assert lib.yrss_set_dispatch_ctx(None) == 0
     buf = ctypes.create_string_buffer(64)
     assert lib.yrss_toeplitz_dispatch(ctypes.cast(buf, ctypes.c_void_p), 64, 0, 3) == -1
+
+
+def test_remote_library_exports_its_header_and_no_hip():
+    """include/yrss_remote.h is the lcore-side library: every declared function
+    is exported, and it does not link the HIP runtime (the lcore holds no GPU
+    context; only the yrss_helper process does)."""
+    from yastack_amd import remote
+
+    remote.load()
+    names = abi.header_functions(abi.REPO_DIR / "include" / "yrss_remote.h")
+    assert len(names) == 6
+    out = subprocess.run(["nm", "-D", "--defined-only", str(remote.LIB_PATH)],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (yrss_\w+)", out))
+    assert not [n for n in names if n not in exported]
+    deps = subprocess.run(["ldd", str(remote.LIB_PATH)], capture_output=True, text=True).stdout
+    assert "amdhip" not in deps and "hsa" not in deps
+    assert remote.HELPER_PATH.exists() and os.access(remote.HELPER_PATH, os.X_OK)

@@ -29,7 +29,8 @@ def _line(stdout):
 
 
 def test_gpus2_spawns_two_ranks():
-    r = _run(["--gpus", "2", "--dry", "--steps", "3", "--warmup", "0", "--pkts", "1000"])
+    r = _run(["--gpus", "2", "--dry", "--steps", "3", "--warmup", "0", "--pkts", "1000",
+              "--cpu-seconds", "0"])
     assert r.returncode == 0, r.stderr
     d = _line(r.stdout)
     assert d["dry"] is True and d["value"] is None
@@ -40,7 +41,7 @@ def test_gpus2_spawns_two_ranks():
 
 
 def test_gpus1_single_rank():
-    r = _run(["--gpus", "1", "--dry", "--steps", "2", "--warmup", "0"])
+    r = _run(["--gpus", "1", "--dry", "--steps", "2", "--warmup", "0", "--cpu-seconds", "0"])
     assert r.returncode == 0, r.stderr
     d = _line(r.stdout)
     assert d["n_gpus"] == 1 and len(d["config"]["devices"]) == 1
@@ -54,7 +55,7 @@ def test_world_size_mismatch_fails():
 
 def test_shared_device_refused():
     # two ranks claiming one device (no rehearsal flag) must not produce a line
-    r = _run(["--gpus", "2", "--dry", "--steps", "1"], {"YRSS_BENCH_FAKE_SAME_DEVICE": "1"})
+    r = _run(["--gpus", "2", "--dry", "--steps", "1", "--cpu-seconds", "0"], {"YRSS_BENCH_FAKE_SAME_DEVICE": "1"})
     assert r.returncode != 0
     assert "share a device" in r.stderr
 
@@ -71,9 +72,32 @@ def test_torchrun_two_ranks():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                         "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "2",
-                        "--dry", "--steps", "2", "--warmup", "0", "--pkts", "500"],
+                        "--dry", "--steps", "2", "--warmup", "0", "--pkts", "500",
+                        "--cpu-seconds", "0"],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and len(set(d["config"]["devices"])) == 2
     assert d["pkts_total"] == 2 * 2 * 500
+
+
+def test_two_ranks_check_and_cpu_baseline():
+    """N > 1 line: bit_exact is the AND over every rank's own shard check (a
+    failing rank 1 turns it false), each rank's result is listed, and the CPU
+    baseline is present at n_gpus 2 (rank 0, after the device work)."""
+    base = ["--gpus", "2", "--dry", "--steps", "2", "--warmup", "0", "--pkts", "4096",
+            "--check", "4096", "--cpu-seconds", "1"]
+    r = _run(base, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2
+    assert d["check"]["bit_exact"] is True and d["check"]["ranks_checked"] == 2
+    assert d["check"]["pkts_checked"] == 2 * 4096
+    assert [x["rank"] for x in d["check"]["per_rank"]] == [0, 1]
+    cpu = d["cpu_baseline"]
+    assert cpu and cpu["value"] > 0 and cpu["cores"] == 1 and cpu["all_cores"]["cores"] >= 1
+    r = _run(base[:-2] + ["--cpu-seconds", "0"], {"YRSS_BENCH_DRY_FAIL_RANK": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert d["check"]["bit_exact"] is False
+    assert [x["bit_exact"] for x in d["check"]["per_rank"]] == [True, False]

@@ -1,15 +1,14 @@
-"""Parity across the parse kernel's work layouts (GPU).
+"""Parity across the work layouts and scatter paths (GPU).
 
-The parse kernel deals chunks of tiles round-robin to its waves, counts per
-chunk, and the scatter works per group of chunks (yrss.hip layout_for).  The
-chunk size depends on the bucket count and on the batch size, and can be forced
-with YRSS_CHUNK_TILES / YRSS_GROUP_TILES (read at yrss_init).  Every layout
-must give the same bit-exact q, hash and per-queue FIFO lists as the oracle
-(fs/lib/ff_dpdk_if.c:1945-2113 and the process_packets enqueue order,
-:1058-1094).
+The parse kernel deals chunks of tiles round-robin to its waves and counts per
+chunk; the scatter ranks and stages each span of chunks itself (yrss.hip
+layout_for, yrss_scatter).  Chunk size, span size, parse grid and the
+XCD-contiguous span mapping are layout choices only (yrss_set_tuning): every
+combination, with the fused protocol_filter on or off, ragged batch sizes and
+window strides 64 and 80, must give the oracle's q, hash and per-queue FIFO
+lists bit-exactly (fs/lib/ff_dpdk_if.c:1945-2113 and the process_packets
+enqueue order, :1058-1094), and no device guard may fire (fault record empty).
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -29,12 +28,20 @@ def to_np(t, dtype):
     return t.cpu().numpy().view(dtype)
 
 
-def check(eng, oracle_mod, cfg_tuple, profile, n, stride=64, first=0):
+KNI = ("accept", "0-32767", "1000-40000,53,123")
+
+
+def check(eng, oracle_mod, cfg_tuple, profile, n, stride=64, first=0, want_filter=False):
+    """One device batch against the oracle: q, hash, qstart, qidx (and the
+    filter class when asked), plus an empty fault record."""
     npr, nq, soft, only = cfg_tuple
+    if want_filter:
+        eng.set_kni(True, *KNI)
     win, lens = eng.synth(profile, n, first, stride=stride)
-    res = eng.dispatch_dev(win, lens, stride, n)
+    res = eng.dispatch_dev(win, lens, stride, n, want_filter=want_filter)
     torch.cuda.synchronize()
-    assert eng.status() == 0   # no scan look-back or scatter guard fired
+    fault = eng.fault_info()
+    assert fault[0] == abi.FAULT_NONE, f"device guard fired: {fault}"
     w_h = win[: n * stride].cpu().numpy()
     l_h = to_np(lens[:n], np.uint16)
     c = oracle_mod.cfg(npr, nq, soft, only)
@@ -45,51 +52,59 @@ def check(eng, oracle_mod, cfg_tuple, profile, n, stride=64, first=0):
     assert bad.size == 0, f"{bad.size} q/hash mismatches, first at {bad[:5]}"
     qi_ref, qs_ref = oracle_mod.process_burst(q_ref, nq)
     assert np.array_equal(to_np(res.qstart, np.uint32), qs_ref)
-    assert np.array_equal(to_np(res.qidx[:n], np.uint32), qi_ref)
+    qi = to_np(res.qidx[:n], np.uint32)
+    d = np.nonzero(qi != qi_ref)[0]
+    assert d.size == 0, f"{d.size} qidx mismatches, first at {d[:5]}: {qi[d[:5]]} vs {qi_ref[d[:5]]}"
+    if want_filter:
+        want = oracle_mod.filter_windows(w_h, stride, l_h, True, oracle_mod.kni_bitmap(KNI[1]),
+                                         oracle_mod.kni_bitmap(KNI[2]))
+        assert np.array_equal(res.filter[:n].cpu().numpy(), want)
+    return res
 
 
-class _env:
-    def __init__(self, **kv):
-        self.kv = {k: str(v) for k, v in kv.items()}
-
-    def __enter__(self):
-        self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update(self.kv)
-
-    def __exit__(self, *a):
-        for k, v in self.old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
-@pytest.mark.parametrize("chunk,group", [(1, 1), (1, 64), (2, 2), (8, 64), (32, 32),
-                                         (4, 256), (128, 128)])
+@pytest.mark.parametrize("want_filter", [False, True])
+@pytest.mark.parametrize("chunk,span", [(1, 1), (1, 64), (2, 2), (8, 64), (32, 32),
+                                        (4, 256), (128, 128)])
 @pytest.mark.parametrize("profile", [abi.SYN_TCP4, abi.SYN_FUZZ])
-def test_forced_layouts(dev, oracle_mod, chunk, group, profile):
-    """Chunk and group sizes are tuning knobs only: results never change."""
+def test_forced_layouts(dev, oracle_mod, chunk, span, profile, want_filter):
+    """Chunk and span sizes are layout choices only: results never change
+    (spans of several pieces and spans of a fraction of a chunk included)."""
     cfg = (5, 5, 1, 1)
-    with _env(YRSS_CHUNK_TILES=chunk, YRSS_GROUP_TILES=group):
-        with SoftRss(*cfg, device=0, max_burst=0) as eng:
-            check(eng, oracle_mod, cfg, profile, 300001, first=777)
-
-
-@pytest.mark.parametrize("cfg", [(32, 32, 1, 0), (100, 100, 1, 1), (17, 17, 1, 0)])
-def test_bucket_count_layouts(dev, oracle_mod, cfg):
-    """Past 17 buckets chunks are 16 tiles while the count slots per wave
-    hold them (yrss.hip layout_for), larger past that."""
     with SoftRss(*cfg, device=0, max_burst=0) as eng:
-        for profile in (abi.SYN_TCP4, abi.SYN_IMIX):
-            check(eng, oracle_mod, cfg, profile, 1 << 20, first=99)
+        eng.set_tuning(chunk_tiles=chunk, span_tiles=span)
+        check(eng, oracle_mod, cfg, profile, 300001, first=777, want_filter=want_filter)
 
 
-@pytest.mark.parametrize("waves", [4, 12, 32])
-def test_occupancy_knob(dev, oracle_mod, waves):
-    """Fewer or more resident waves change the deal (chunks per wave), not results."""
-    cfg = (3, 3, 1, 1)
-    with _env(YRSS_WAVES_PER_CU=waves):
+@pytest.mark.parametrize("stride", [64, 80])
+@pytest.mark.parametrize("want_filter", [False, True])
+@pytest.mark.parametrize("n", [4097, 5000, 77777, 1 << 20])
+@pytest.mark.parametrize("cfg", [(2, 2, 1, 0), (3, 3, 1, 1), (8, 8, 1, 0), (16, 16, 1, 1),
+                                 (64, 64, 1, 0), (255, 255, 1, 0), (4096, 256, 1, 1)])
+def test_bucket_counts(dev, oracle_mod, cfg, n, want_filter, stride):
+    """2 to 257 buckets, ragged sizes, filter on and off, strides 64 and 80."""
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        for profile in (abi.SYN_FUZZ, abi.SYN_IMIX):
+            check(eng, oracle_mod, cfg, profile, n, stride=stride, first=n + 99,
+                  want_filter=want_filter)
+
+
+@pytest.mark.parametrize("cfg", [(8, 8, 1, 0), (8, 8, 1, 1)])
+def test_filter_parity_fuzz_lists(dev, oracle_mod, cfg):
+    """The configuration of round 2's faulted run (9 buckets, the fused
+    filter, stride 64, n = 60001, fuzz then IMIX in one context), lists and
+    fault record included."""
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        for profile in (abi.SYN_FUZZ, abi.SYN_IMIX):
+            check(eng, oracle_mod, cfg, profile, 60001, first=99, want_filter=True)
+
+
+@pytest.mark.parametrize("blocks", [1, 7, 64, 1000])
+def test_parse_grid(dev, oracle_mod, blocks):
+    """Fewer or more parse workgroups change the deal (chunks per wave and,
+    with few waves, larger chunks so the count slots fit), not results."""
+    for cfg in ((3, 3, 1, 1), (100, 100, 1, 1)):
         with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            eng.set_tuning(parse_blocks=blocks)
             check(eng, oracle_mod, cfg, abi.SYN_IMIX, 1 << 21, first=5)
 
 
@@ -101,23 +116,20 @@ def test_batch_beyond_default_chunks(dev, oracle_mod):
         check(eng, oracle_mod, cfg, abi.SYN_TCP4, 1 << 26, first=3)
 
 
-@pytest.mark.parametrize("cfg", [(9, 9, 1, 0), (32, 32, 1, 0), (4096, 256, 1, 1)])
-def test_ballot_scatter_without_ranks(dev, oracle_mod, cfg):
-    """YRSS_NO_RANK=1 keeps many-bucket batches on the ballot-ranked scatter
-    (no per-packet ranks from the parse kernel); same lists either way."""
-    with _env(YRSS_NO_RANK=1):
-        with SoftRss(*cfg, device=0, max_burst=0) as eng:
-            check(eng, oracle_mod, cfg, abi.SYN_FUZZ, 500001, first=11)
+@pytest.mark.parametrize("cfg", [(255, 255, 1, 0), (64, 64, 1, 1)])
+def test_many_buckets_large_chunks(dev, oracle_mod, cfg):
+    """Many buckets at 2^25 packets: chunks past the span size (a span is
+    then one chunk, worked in several pieces)."""
     with SoftRss(*cfg, device=0, max_burst=0) as eng:
-        check(eng, oracle_mod, cfg, abi.SYN_FUZZ, 500001, first=11)
+        check(eng, oracle_mod, cfg, abi.SYN_TCP4, 1 << 25, first=17)
 
 
 @pytest.mark.parametrize("profile", [abi.SYN_UDP4, abi.SYN_TCP4, abi.SYN_IMIX])
 @pytest.mark.parametrize("shift", [1, 2, 3])
 def test_unaligned_list_outputs(oracle_mod, profile, shift):
     """qidx (and q / hash) at 4-byte but not 16-byte alignment, n not a
-    multiple of 4: the list paths' unaligned heads and tails (one-list
-    grid-stride path on UDP, LDS-image path on TCP / IMIX)."""
+    multiple of 4: the lists' 16-byte quads follow the address, not the index
+    (one-list path on UDP, staged scatter on TCP / IMIX)."""
     n, stride = 300007, 64
     with SoftRss(3, 3, 1, 1, device=0, max_burst=0) as eng:
         win, lens = eng.synth(profile, n, 17, stride=stride)
@@ -131,6 +143,7 @@ def test_unaligned_list_outputs(oracle_mod, profile, shift):
                              qi_buf[shift:shift + n], qs)
         res = eng.dispatch_dev(win, lens, stride, n, out=out)
         torch.cuda.synchronize()
+        assert eng.status() == 0
         w_h = win[: n * stride].cpu().numpy()
         l_h = lens[:n].cpu().numpy().view(np.uint16)
         q_ref, h_ref = oracle_mod.dispatch_windows(w_h, stride, l_h, oracle_mod.cfg(3, 3, 1, 1))
@@ -144,26 +157,18 @@ def test_unaligned_list_outputs(oracle_mod, profile, shift):
 
 
 @pytest.mark.parametrize("xcd", [0, 1])
-@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (8, 8, 1, 0), (16, 16, 1, 0), (48, 48, 1, 0),
-                                 (64, 64, 1, 1), (255, 255, 1, 0)])
+@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (8, 8, 1, 0), (48, 48, 1, 0), (255, 255, 1, 0)])
 def test_scatter_xcd_mapping(dev, oracle_mod, cfg, xcd):
-    """YRSS_SCATTER_XCD moves scatter groups between workgroups (XCD-contiguous
-    or round-robin; default by bucket count): every path's lists are the same,
-    including ragged grids (n not a multiple of a group)."""
-    with _env(YRSS_SCATTER_XCD=xcd):
-        with SoftRss(*cfg, device=0, max_burst=0) as eng:
-            for profile in (abi.SYN_TCP4, abi.SYN_FUZZ):
-                check(eng, oracle_mod, cfg, profile, 777777, first=31)
+    """XCD-contiguous or round-robin spans: the same lists, ragged grids
+    included (n not a multiple of a span)."""
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.set_tuning(scatter_xcd=xcd)
+        for profile in (abi.SYN_TCP4, abi.SYN_FUZZ):
+            check(eng, oracle_mod, cfg, profile, 777777, first=31)
 
 
-@pytest.mark.parametrize("group", [16, 32, 64])
-@pytest.mark.parametrize("cfg", [(7, 7, 1, 0), (8, 8, 1, 0), (12, 12, 1, 1), (16, 16, 1, 0), (48, 48, 1, 0),
-                                 (100, 100, 1, 1), (255, 255, 1, 0), (4096, 256, 1, 1)])
-def test_ranked_group_stage(dev, oracle_mod, cfg, group):
-    """YRSS_RANK_GSTAGE: the ranked scatter sorts a whole group in one packed
-    LDS stage (YRSS_RANK_IMG=0 so it also runs at 49 buckets); same lists for
-    any group size, ragged and small batches included."""
-    with _env(YRSS_RANK_GSTAGE=1, YRSS_RANK_IMG=0, YRSS_GROUP_TILES=group):
-        with SoftRss(*cfg, device=0, max_burst=0) as eng:
-            for profile, n in ((abi.SYN_TCP4, 1 << 20), (abi.SYN_FUZZ, 777777), (abi.SYN_IMIX, 5001)):
-                check(eng, oracle_mod, cfg, profile, n, first=47)
+def test_tuning_rejects_bad_values(dev):
+    with SoftRss(3, device=0, max_burst=0) as eng:
+        for kw in ({"chunk_tiles": 3}, {"span_tiles": 6}, {"one_launch": 3}, {"scatter_xcd": 2}):
+            with pytest.raises(abi.YrssError):
+                eng.set_tuning(**kw)

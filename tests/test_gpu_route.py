@@ -45,6 +45,11 @@ def test_filter_parity_fuzz(oracle_mod, kcfg, stride):
             q_ref, h_ref = oracle_mod.dispatch_windows(w_h, stride, l_h, oracle_mod.cfg(8, 8, 1, 0))
             assert np.array_equal(to_np(res.q[:n], np.int16), q_ref)
             assert np.array_equal(to_np(res.hash[:n], np.uint32), h_ref)
+            # and the per-queue lists, with no device guard fired
+            assert eng.fault_info()[0] == abi.FAULT_NONE
+            qi_ref, qs_ref = oracle_mod.process_burst(q_ref, 8)
+            assert np.array_equal(to_np(res.qstart, np.uint32), qs_ref)
+            assert np.array_equal(to_np(res.qidx[:n], np.uint32), qi_ref)
             if enable and (tcp or udp) and profile == abi.SYN_FUZZ:
                 assert (want == abi.FILTER_KNI).sum() > 0 and (want == abi.FILTER_ARP).sum() > 0
 
@@ -75,6 +80,7 @@ def test_filter_ipip_and_edges(oracle_mod):
                                    torch.from_numpy(l_h.view(np.int16)).cuda(), stride, n,
                                    want_filter=True)
             torch.cuda.synchronize()
+            assert eng.status() == 0
             assert np.array_equal(res.filter[:n].cpu().numpy(), want)
 
 
@@ -182,3 +188,7 @@ def test_from_ff_config_kni(oracle_mod, tmp_path):
         assert np.array_equal(res.filter[:n].cpu().numpy(), want)
         q_ref, _ = oracle_mod.dispatch_windows(w_h, stride, l_h, oracle_mod.cfg(4, 4, 1, 1))
         assert np.array_equal(to_np(res.q[:n], np.int16), q_ref)
+        assert eng.status() == 0
+        qi_ref, qs_ref = oracle_mod.process_burst(q_ref, 4)
+        assert np.array_equal(to_np(res.qstart, np.uint32), qs_ref)
+        assert np.array_equal(to_np(res.qidx[:n], np.uint32), qi_ref)

@@ -3,7 +3,6 @@ and nb_queues + 1 <= 64) against the oracle, on every host-resident entry
 point, at sizes on both sides of the threshold.  The multi-kernel path
 (YRSS_NO_SMALL=1) must give identical results.
 """
-import os
 
 import numpy as np
 import pytest
@@ -140,16 +139,16 @@ def test_small_burst_fault_reported(dev, oracle_mod):
 def test_small_and_multi_kernel_paths_agree(dev, oracle_mod, n, monkeypatch):
     frames = _frames(oracle_mod, n, 4242)
     outs = []
-    for no_small in ("0", "1"):
-        monkeypatch.setenv("YRSS_NO_SMALL", no_small)
+    for one_launch in (0, 2):   # default / never (multi-kernel path)
         with SoftRss(3, 3, 1, 1, device=0, max_burst=0) as eng:
+            eng.set_tuning(one_launch=one_launch)
             outs.append(eng.dispatch_frames(frames))
+            assert eng.status() == 0
     a, b = outs
     for f in ("q", "hash", "qidx", "qstart"):
         assert np.array_equal(np.asarray(getattr(a, f)), np.asarray(getattr(b, f))), f
     q, h, qi, qs = _expect(oracle_mod, frames, (3, 3, 1, 1))
     _check(a, q, h, qi, qs)
-    assert os.environ.get("YRSS_NO_SMALL") == "1"
 
 
 @pytest.mark.parametrize("n", [1000, 6000])   # one-launch path / multi-kernel path
@@ -248,9 +247,9 @@ def test_device_batch_small_path(dev, oracle_mod, monkeypatch, n, stride):
     the oracle's."""
     cfg = (5, 4, 1, 1)
     outs = []
-    for small in ("1", "0"):
-        monkeypatch.setenv("YRSS_SMALL_DEV", small)
+    for one_launch in (0, 1):   # device batches in one launch / through the batch kernels
         with SoftRss(*cfg, device=0, max_burst=0) as eng:
+            eng.set_tuning(one_launch=one_launch)
             eng.set_kni(True, "reject", "80,443", "53")
             win, lens = eng.synth(abi.SYN_FUZZ, n, 77, stride=stride)
             r = eng.dispatch_dev(win, lens, stride, n, want_filter=True)

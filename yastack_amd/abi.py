@@ -30,6 +30,11 @@ F_WRITE_RSS = 0x1
 F_ASYNC = 0x2
 
 K_PARSE_HASH, K_SCAN, K_SCATTER = 0, 1, 2
+K_BURST, K_WORKER = 8, 9            # kernel ids of fault records only
+
+# device-side fault record codes (yrss_fault_info)
+FAULT_NONE, FAULT_SCAN_TIMEOUT, FAULT_LIST_RANGE, FAULT_COUNT_MISMATCH, FAULT_COUNT_SLOT, \
+    FAULT_STAGE = range(6)
 
 # protocol_filter classes (ff_dpdk_kni.h:34-38) + boundary outcomes
 FILTER_UNKNOWN, FILTER_ARP, FILTER_KNI, FILTER_TRUNC, FILTER_LOOP = -1, 1, 2, -2, -3
@@ -48,6 +53,11 @@ SYN_NAMES = {
     SYN_VLAN6_TCP: "vlan6_tcp", SYN_JUMBO_TCP4: "jumbo_tcp4", SYN_TCP4: "tcp4",
     SYN_FUZZ: "fuzz",
 }
+
+
+# Fault records (code, kernel, where, value) found unread when a SoftRss
+# context closed: tests fail on any entry (tests/conftest.py).
+FAULT_LOG: list = []
 
 
 class YrssLibraryError(RuntimeError):
@@ -121,6 +131,26 @@ class RouteResult(ctypes.Structure):
     ]
 
 
+class Fault(ctypes.Structure):
+    _fields_ = [
+        ("code", ctypes.c_uint32),
+        ("kernel", ctypes.c_uint32),
+        ("where", ctypes.c_uint32),
+        ("value", ctypes.c_uint32),
+    ]
+
+
+class Tuning(ctypes.Structure):
+    """Layout overrides (yrss_set_tuning); zero fields are the defaults."""
+    _fields_ = [
+        ("chunk_tiles", ctypes.c_uint32),
+        ("span_tiles", ctypes.c_uint32),
+        ("parse_blocks", ctypes.c_uint32),
+        ("one_launch", ctypes.c_uint32),
+        ("scatter_xcd", ctypes.c_int32),
+    ]
+
+
 class SynthParams(ctypes.Structure):
     _fields_ = [
         ("seed", ctypes.c_uint64),
@@ -150,6 +180,8 @@ _PROTOS = {
                                             ctypes.POINTER(ctypes.c_double)]),
     "yrss_grid_for": (_u32, [_vp, _u32]),
     "yrss_status": (ctypes.c_int, [_vp]),
+    "yrss_fault_info": (ctypes.c_int, [_vp, ctypes.POINTER(Fault)]),
+    "yrss_set_tuning": (ctypes.c_int, [_vp, ctypes.POINTER(Tuning)]),
     "yrss_wait": (ctypes.c_int, [_vp]),
     "yrss_worker_start": (ctypes.c_int, [_vp, _u32, _u32]),
     "yrss_worker_submit": (ctypes.c_int, [_vp, _vp, _u32, _vp, _vp, _vp, _vp, _u32,

@@ -48,34 +48,22 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kTile = 64;              // packets per wave-tile (one per lane)
-constexpr int kScatterBlock = 256;     // 4 waves (segments) per workgroup
+constexpr int kScatterBlock = 256;     // 4 waves per scatter workgroup (halved for large nb)
 constexpr int kScatterWaves = kScatterBlock / kWave;
-constexpr int kMaxWavesPerCU = 32;
 constexpr uint32_t kMaxChunks = 65536;  // per launch; bounds the count matrix [nb][ncol]
 constexpr uint32_t kCntWords = 2048;    // parse: per-wave LDS count slots (chunks x nb)
 constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
-constexpr int kScatterRound = 8;       // packets per lane per scatter round
-constexpr uint32_t kFewBuckets = 8;    // scatter: SGPR-cursor path up to this many buckets
-constexpr uint32_t kRankStage = 1024;   // ranked scatter: chunk stage (packets) per wave
-constexpr uint32_t kImgPkts = 4096;     // few-bucket scatter: largest group built in LDS
-constexpr uint32_t kImgLine = 32;       // entries per 128-byte line
-constexpr uint32_t kCntStride = 65;     // count mode: words per bucket's lane counters
-constexpr uint32_t kRankImgMaxNb = 65;  // ranked scatter: LDS image up to this many buckets
-constexpr uint32_t kRankImgMaxNbRr = 33; // the same with round-robin (not XCD-contiguous) groups
-// Toeplitz key tables: the 96 tuple bits are cut into fields of kHashBits
-// (MSB first); table t maps a field value to the XOR of the key windows its
-// set bits select.  8: 12 byte tables of 256 words (12 lookups; random indices
-// over 8 rows of the 32 banks a ds_read_b32 half-wave uses, ~4-way
-// conflicts).  4: 24 nibble tables of 16 words (24 lookups; a table spans 16
-// distinct banks, so a half-wave's reads never conflict).
-#ifndef YRSS_HASH_BITS
-#define YRSS_HASH_BITS 8
-#endif
-constexpr int kHashBits = YRSS_HASH_BITS;
-static_assert(kHashBits == 4 || kHashBits == 8, "field width divides 32");
-constexpr int kFieldsPerWord = 32 / kHashBits;
-constexpr int kTblEntries = 1 << kHashBits;
-constexpr int kTblWordsPerTupleWord = kFieldsPerWord * kTblEntries;
+constexpr uint32_t kPiece = 2048;       // scatter: packets ranked and staged at once per wave
+constexpr uint32_t kPieceSlots = kPiece / 64;   // 64-packet slots of a piece
+constexpr uint32_t kImgLine = 32;       // list entries per 128-byte line
+constexpr uint32_t kTab = 16;           // ranked scatter: prefix-table words per lane (nb x 2nc <= 1024)
+// Toeplitz key tables: the 96 tuple bits are cut into 12 bytes (MSB first);
+// table t maps a byte value to the XOR of the key windows its set bits select
+// (12 lookups per hash).  Nibble tables (24 conflict-free lookups) and
+// bit-serial VALU words were measured and gave nothing (profiles/r02_v1_*,
+// r01_v29_*): the parse kernel is bound by its HBM stream, not the hash.
+constexpr int kTblEntries = 256;
+constexpr int kTblWordsPerTupleWord = 4 * kTblEntries;
 constexpr int kTblWords = 3 * kTblWordsPerTupleWord;
 constexpr int kTblBytes = kTblWords * 4;
 constexpr int kRsrcWord3 = 0x00020000;  // buffer resource dword 3 for gfx9-family (CDNA)
@@ -91,9 +79,9 @@ struct ParseParams {
     uint32_t *hash;       // may be null
     uint32_t *seg_cnt;    // [nb][ncol] per-chunk counts, bucket-major, or null
     uint16_t *rank;       // kCount == 2: packet's rank among its chunk's same-bucket packets
+    uint32_t *fault;      // host-coherent fault record (report_fault), or null
     uint32_t n;
     uint32_t stride;
-    uint32_t seg;         // unused by the parse kernel (scatter group size)
     uint32_t chunk;       // packets per chunk (dealt round-robin to waves), multiple of kTile
     uint32_t nchunk;      // chunks in this launch
     uint32_t ncol;        // row stride of seg_cnt (chunk columns, padded)
@@ -102,12 +90,11 @@ struct ParseParams {
     uint32_t nb;          // buckets = nq + 1 (last = drop)
     uint32_t mod_d;       // divisor: nb_procs or nb_procs-1
     uint32_t q_off;       // 0 or 1 (dispatch_only_core)
-    uint32_t nseg;        // unused by the parse kernel
     uint64_t mod_m;       // Lemire fastmod constant for mod_d
     int8_t *filter;       // protocol_filter class per packet, or null
     const uint32_t *kni_bm;   // tcp bitmap (2048 words) then udp bitmap (2048 words)
     uint32_t kni_enable;
-    uint32_t out16;       // q/hash bursts as 16-byte stores: 1 plain, 2 sc1 (YRSS_OUT16)
+    uint32_t out16;       // full output bursts as 16-byte write-through stores (0: lane-granular)
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
@@ -117,26 +104,39 @@ struct ScatterParams {
     const uint32_t *totals;    // [nb]
     uint32_t *qidx;
     uint32_t *qstart;          // [nb + 1]
+    uint32_t *fault;           // host-coherent fault record
     uint32_t n;
-    uint32_t seg;
+    uint32_t seg;              // packets per span (one wave's unit: 2^gshift chunks)
     uint32_t nq;
     uint32_t nb;
-    uint32_t nseg;             // groups (one scatter wave each)
     uint32_t nchunk;           // chunk columns written by the parse kernel
     uint32_t ncol;             // row stride of seg_off
-    uint32_t gshift;           // a group is 2^gshift chunks
-    uint32_t chunk;            // packets per chunk
+    uint32_t gshift;           // a span is 2^gshift chunks
+    uint32_t cshift;           // a chunk is 2^cshift packets
     const uint16_t *rank;      // ranked mode: rank in chunk per packet (parse kCount == 2)
-    uint32_t img;              // words of a wave's LDS list image (0: per-lane stores)
-    uint32_t single;           // a batch feeding one list takes the grid-stride identity path
-    uint32_t aux;              // words of a wave's LDS cursors ahead of its image
+    uint32_t aux;              // words of a wave's per-bucket arrays ahead of its stage
+    uint32_t stg;              // words of a wave's stage (kPiece + 3 per bucket, rounded)
     uint32_t wlds;             // words of LDS per wave
-    uint32_t cnt_off;          // count mode: wave LDS word offset of its counters (0: off)
-    uint32_t kmin;             // count mode for groups feeding more than kmin buckets
-    uint32_t xcd;              // workgroups of one XCD take consecutive groups (xcd_block)
-    uint32_t gstage;           // ranked stage path: one packed stage per group, not per chunk
-    uint32_t *fault;           // host-coherent fault word (the scan's): a guard that fired
+    uint32_t xcd;              // workgroups of one XCD take consecutive spans (xcd_block)
 };
+
+// Device-side fault record in host-coherent memory: {code, kernel, where,
+// value}, the first fault of a batch wins (yrss_status / yrss_fault_info).
+// Every guard on a rank-, count- or cursor-driven index reports here instead
+// of storing, so a disagreement can neither fault the GPU nor pass silently.
+__device__ __forceinline__ void report_fault(uint32_t *rec, uint32_t code, uint32_t kernel,
+                                          uint32_t where, uint32_t value)
+{
+    if (!rec)
+        return;
+    uint32_t expected = 0u;
+    if (__hip_atomic_compare_exchange_strong(rec, &expected, code, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+        __hip_atomic_store(rec + 1, kernel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(rec + 2, where, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(rec + 3, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
@@ -160,6 +160,14 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// x, hidden from the optimiser: per-lane offsets derived from it inside a loop
+// are recomputed there (a few VALU) instead of hoisted out and spilled
+__device__ __forceinline__ uint32_t opaque(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
 }
 
 __device__ __forceinline__ uint64_t lane_lt_mask(uint32_t lane)
@@ -226,70 +234,30 @@ __device__ __forceinline__ uint32_t win_byte(const ParseParams &P, const uint32_
     return 0u;
 }
 
-// FilterReturn values (ff_dpdk_kni.h:34-38) plus the two boundary outcomes.
-// Toeplitz over one 32-bit tuple word (bit 31-k selects key window k), the two
-// ways: four lookups into byte tables tb[j*256+v] (v = byte j of the word from
-// the top), or bit-serial on the VALU with the windows in SGPRs.
-__device__ __forceinline__ uint32_t field_of(uint32_t w, int f)
-{
-    const int pos = 32 - (f + 1) * kHashBits;
-    if constexpr (kHashBits == 8)
-        return (w >> pos) & 0xffu;
-    // v_bfe_u32 by hand: left to itself the compiler turns (w >> pos) & 15
-    // into a pre-scaled (w >> (pos-2)) & 60 and then cannot fold the LDS base
-    // into v_lshl_add_u32, one VALU op more per lookup
-    uint32_t x;
-    asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(x) : "v"(w), "i"(pos), "i"(kHashBits));
-    return x;
-}
-
+// Toeplitz over one 32-bit tuple word (bit 31-k selects key window k): four
+// lookups into byte tables tb[j*256 + v], v = byte j of the word from the top.
 __device__ __forceinline__ uint32_t tz_lds(uint32_t w, const uint32_t *tb)
 {
-    uint32_t v[kFieldsPerWord];
-#pragma unroll
-    for (int f = 0; f < kFieldsPerWord; ++f)
-        v[f] = tb[f * kTblEntries + field_of(w, f)];
-    if constexpr (kFieldsPerWord == 4) {
-        return v[0] ^ v[1] ^ v[2] ^ v[3];
-    } else {   // 8 nibble lookups: xor3 tree (v_bitop3 0x96)
-        const uint32_t a = __builtin_amdgcn_bitop3_b32(v[0], v[1], v[2], 0x96);
-        const uint32_t b = __builtin_amdgcn_bitop3_b32(v[3], v[4], v[5], 0x96);
-        return __builtin_amdgcn_bitop3_b32(a, b, v[6] ^ v[7], 0x96);
-    }
+    return tb[(w >> 24) & 0xffu] ^ tb[256 + ((w >> 16) & 0xffu)] ^
+           tb[512 + ((w >> 8) & 0xffu)] ^ tb[768 + (w & 0xffu)];
 }
 
-// Table t, value v: XOR of key windows kwin[t*kHashBits + b] over v's set
-// bits b (b = 0 is v's most significant bit).  Threads tid, tid+nthr, ...
+// Table t, value v: XOR of key windows kwin[8t + b] over v's set bits b (b = 0
+// is v's most significant bit).  Threads tid, tid + nthr, ...
 __device__ __forceinline__ void build_key_tables(uint32_t *tbl, const uint32_t *kwin,
                                                  uint32_t tid, uint32_t nthr)
 {
     for (uint32_t e = tid; e < (uint32_t)kTblWords; e += nthr) {
-        const uint32_t t = e >> kHashBits, v = e & (kTblEntries - 1u);
+        const uint32_t t = e >> 8, v = e & 0xffu;
         uint32_t acc = 0;
 #pragma unroll
-        for (int b = 0; b < kHashBits; ++b)
-            acc ^= (v & (1u << (kHashBits - 1 - b))) ? kwin[kHashBits * t + b] : 0u;
+        for (int b = 0; b < 8; ++b)
+            acc ^= (v & (0x80u >> b)) ? kwin[8 * t + b] : 0u;
         tbl[e] = acc;
     }
 }
 
-__device__ __forceinline__ uint32_t tz_valu(uint32_t w, const uint32_t *kw, uint32_t h)
-{
-#pragma unroll
-    for (int k = 0; k < 32; ++k)   // h ^= (bit ? ~0 : 0) & kw[k]  (truth table 0x6a)
-        h = __builtin_amdgcn_bitop3_b32((uint32_t)((int32_t)(w << k) >> 31), kw[k], h, 0x6a);
-    return h;
-}
-
-#ifndef YRSS_CNT_WG
-#define YRSS_CNT_WG 1   // parse count slots flushed by the workgroup, 8 columns per row
-#endif
-
-#ifndef YRSS_VALU_WORDS
-#define YRSS_VALU_WORDS 0
-#endif
-constexpr int kVw = YRSS_VALU_WORDS;   // tuple words hashed on the VALU (0..3)
-
+// FilterReturn values (ff_dpdk_kni.h:34-38) plus the two boundary outcomes.
 constexpr int kFilterUnknown = -1, kFilterArp = 1, kFilterKni = 2;
 constexpr int kFilterTrunc = -2;   // header walk left the staged window
 constexpr int kFilterLoop = -3;    // IPIP with IHL=0: the reference recurses forever
@@ -358,7 +326,7 @@ struct OutSlot {
 // remainder keeps the lane-granular stores.
 // Buffer resources sized to the valid bytes drop lanes past the end, so every
 // store issues and the vmcnt bookkeeping stays exact.
-template <bool kFilter, bool kRank>
+template <bool kFilter, bool kRank = false>
 __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *oq,
                                           const uint32_t *oh, const int8_t *of,
                                           const uint16_t *orank, uint32_t t_first,
@@ -371,24 +339,17 @@ __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *
         P.hash ? (void *)(P.hash + t_first) : (void *)P.q, 0, P.hash ? (int)(nv * 4u) : 0,
         kRsrcWord3);
     if (P.out16 && nv == ntiles * (uint32_t)kTile) {
-        // a whole batch of tiles: 16-byte stores, 1 KiB of hash and 512 B of
-        // q per wave-instruction at 4 tiles; out16 == 2 stores write-through
-        // (sc1: the lines leave L2 at once, none is left dirty at kernel end)
+        // a whole batch of tiles: 16-byte write-through (sc1) stores, 1 KiB of
+        // hash and 512 B of q per wave-instruction at 4 tiles; the lines leave
+        // L2 at once, none is left dirty at kernel end
         wave_lds_sync();
         const uint32_t nh = nv >> 2, nq8 = nv >> 3;
         const u32x4 vh = *reinterpret_cast<const u32x4 *>(oh + 4u * min(lane, nh - 1u));
         const u32x4 vq = *reinterpret_cast<const u32x4 *>(oq + 8u * min(lane, nq8 - 1u));
-        if (P.out16 == 2) {
-            if (lane < nh)
-                __builtin_amdgcn_raw_buffer_store_b128(vh, rh, (int)(lane * 16u), 0, 16);
-            if (lane < nq8)
-                __builtin_amdgcn_raw_buffer_store_b128(vq, rq, (int)(lane * 16u), 0, 16);
-        } else {
-            if (lane < nh)
-                __builtin_amdgcn_raw_buffer_store_b128(vh, rh, (int)(lane * 16u), 0, 0);
-            if (lane < nq8)
-                __builtin_amdgcn_raw_buffer_store_b128(vq, rq, (int)(lane * 16u), 0, 0);
-        }
+        if (lane < nh)
+            __builtin_amdgcn_raw_buffer_store_b128(vh, rh, (int)(lane * 16u), 0, 16);
+        if (lane < nq8)
+            __builtin_amdgcn_raw_buffer_store_b128(vq, rq, (int)(lane * 16u), 0, 16);
         wave_lds_sync();
     } else {
         for (uint32_t j = 0; j < ntiles; ++j) {
@@ -471,24 +432,12 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
         // Tuple = LE image of ntohl(src), ntohl(dst), ntohs(sport), ntohs(dport)
         // (ff_dpdk_if.c:1994-2021).
         // Tuple words in key order: w0 = saddr, w1 = daddr, w2 = ports; bit 31-k of
-        // wi selects key window 32i+k.  Word i < kVw runs bit-serial on the VALU
-        // (bfe + one 3-input bitop per bit), the rest as 4 byte-table lookups.
+        // wi selects key window 32i+k; each word is 4 byte-table lookups.
         const uint32_t w0 = __builtin_amdgcn_alignbit(d7, d6, 16);
         const uint32_t w1 = __builtin_amdgcn_alignbit(d8, d7, 16);
-        uint32_t h_l3 = 0;
         const uint32_t w2 = (pa & 0xffff0000u) | (pb & 0xffffu);
-        if (kVw > 0)
-            h_l3 = tz_valu(w0, P.kwin, h_l3);
-        else
-            h_l3 = tz_lds(w0, tbl);
-        if (kVw > 1)
-            h_l3 = tz_valu(w1, P.kwin + 32, h_l3);
-        else
-            h_l3 ^= tz_lds(w1, tbl + kTblWordsPerTupleWord);
-        if (kVw > 2)
-            h = tz_valu(w2, P.kwin + 64, h_l3);
-        else
-            h = h_l3 ^ tz_lds(w2, tbl + 2 * kTblWordsPerTupleWord);
+        const uint32_t h_l3 = tz_lds(w0, tbl) ^ tz_lds(w1, tbl + kTblWordsPerTupleWord);
+        h = h_l3 ^ tz_lds(w2, tbl + 2 * kTblWordsPerTupleWord);
         bool trunc = false;
         // Rare slow path, entered only by waves that hold such a packet, so its
         // global loads (and the vmcnt drain they imply) stay off the hot loop.
@@ -553,7 +502,8 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
         // with ceil(log2 nb) ballots (match-any by bit slices); the lowest
         // lane of each group adds the group size.  Cost is independent of how
         // many distinct buckets the tile holds.  kCount == 2 also keeps each
-        // packet's rank among the chunk's packets of its bucket: the leader's
+        // packet's rank among the chunk's (one-launch kernels: the tile's)
+        // packets of its bucket: the leader's
         // atomic returns the count before the group (a wave's LDS atomics run
         // in issue order, so tiles stay in packet order) and each lane adds
         // its position inside the group.
@@ -575,14 +525,17 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
 
 // ---------------------------------------------------------------------------
 // Kernel 1 entry.
-//   kCount   also count packets per bucket per wave segment (compaction on)
+//   kCount   1: also count packets per bucket per chunk (per-queue lists on);
+//            2: and write each packet's rank among its chunk's packets of its
+//            bucket (the ranked scatter places packets by it)
 //   kFilter  also classify protocol_filter / KNI (one byte per packet)
-//   kNT      non-temporal (streaming) window loads
 //   kBlock   workgroup size (256/512): waves per CU, one key table per group
+// Window loads are non-temporal (streaming): ~25 % faster than default-policy
+// loads (profiles/r01_v32_nt_ab.log).
 // LDS: key tables 12 KiB | staging 4 KiB per wave | count slots 8 KiB per wave |
-//      output buffer 1.75 KiB per wave | KNI bitmaps 16 KiB (kFilter only).
+//      output buffer 2.25 KiB per wave | KNI bitmaps 16 KiB (kFilter only).
 // ---------------------------------------------------------------------------
-template <int kCount, bool kFilter, bool kNT, int kBlock>
+template <int kCount, bool kFilter, int kBlock>
 __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
 {
     constexpr int kWaves = kBlock / kWave;
@@ -628,6 +581,19 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     // register sets, unrolled by two, so no copy at the latch waits on a load;
     // the look-ahead load always issues (it re-reads the current tile at the
     // end) so the wait counts are the same on every path.
+    // The host sizes chunks so a wave's slots fit (layout_for); a wave that
+    // would own more chunks than it has slots reports and does nothing (the
+    // check sits outside the loop: a fault-report branch inside it cost the
+    // loop's load scheduling)
+    bool slots_ok = true;   // (the wave still takes part in the workgroup's barriers)
+    if (kCount) {
+        const uint32_t own = P.nchunk > gw ? (P.nchunk - gw + W - 1u) / W : 0u;
+        if (own * P.nb > kCntWords) {
+            slots_ok = false;
+            if (lane == 0)
+                report_fault(P.fault, YRSS_FAULT_COUNT_SLOT, YRSS_K_PARSE_HASH, gw, own);
+        }
+    }
     auto tile_at = [&](uint32_t i, uint32_t &t0, uint32_t &slot) -> bool {
         const uint32_t kk = i >> P.ct_shift;
         const uint64_t c = gw + (uint64_t)kk * W;
@@ -648,37 +614,40 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     auto after = [&](uint32_t i, uint32_t t0, bool last) {
         if (((i + 1u) & fb_mask) == 0u || last)
             flush_out<kFilter, kCount == 2>(P, oq, oh, of, orank, t0 - (i & fb_mask) * kTile,
-                                             (i & fb_mask) + 1u, lane);
+                                            (i & fb_mask) + 1u, lane);
     };
+    constexpr int kC = kCount;
     uint32_t tA = 0, sA = 0, tB = 0, sB = 0;
-    if (tile_at(0, tA, sA)) {
+    if (slots_ok && tile_at(0, tA, sA)) {
         u32x4 rA[4], rB[4];
         uint32_t LA, LB;
-        load_tile<kNT>(P, tA, P.n, lane, rA, LA);
+        load_tile<true>(P, tA, P.n, lane, rA, LA);
         for (uint32_t i = 0;; i += 2) {
             const bool hB = tile_at(i + 1, tB, sB);
-            load_tile<kNT>(P, hB ? tB : tA, P.n, lane, rB, LB);
-            process_tile<kCount, kFilter>(P, tbl, kni, stage, cnt_w + sA * P.nb, slot(i), tA,
-                                          P.n, lane, rA, LA);
+            load_tile<true>(P, hB ? tB : tA, P.n, lane, rB, LB);
+            process_tile<kC, kFilter>(P, tbl, kni, stage, cnt_w + sA * P.nb, slot(i), tA, P.n,
+                                      lane, rA, LA);
             after(i, tA, !hB);
             if (!hB)
                 break;
             const bool hA = tile_at(i + 2, tA, sA);
-            load_tile<kNT>(P, hA ? tA : tB, P.n, lane, rA, LA);
-            process_tile<kCount, kFilter>(P, tbl, kni, stage, cnt_w + sB * P.nb, slot(i + 1),
-                                          tB, P.n, lane, rB, LB);
+            load_tile<true>(P, hA ? tA : tB, P.n, lane, rA, LA);
+            process_tile<kC, kFilter>(P, tbl, kni, stage, cnt_w + sB * P.nb, slot(i + 1), tB,
+                                      P.n, lane, rB, LB);
             after(i + 1, tB, !hA);
             if (!hA)
                 break;
         }
     }
-    if (kCount && YRSS_CNT_WG) {
+    if (kCount) {
         // Workgroup flush: for its j-th chunk each of the 8 waves owns column
         // blockIdx.x * 8 + w + j * W, so the workgroup's columns of round j
         // are 8 consecutive words of every bucket row.  Thread e takes wave
         // e % 8, bucket (e / 8) % nb, round e / (8 nb): a 64-lane store then
         // covers 8 rows x 32 contiguous bytes instead of one word in each of
-        // 64 rows (a store costs the lines its lanes touch).
+        // 64 rows (a store costs the lines its lanes touch; the per-wave flush
+        // it replaced cost 2 us on UDP and 33 us at 256 buckets,
+        // profiles/r02_v30_cntwg_ab.log).
         __syncthreads();
         const uint32_t g0 = blockIdx.x * kWaves;
         const uint32_t kmax = P.nchunk > g0 ? (P.nchunk - g0 + W - 1) / W : 0u;
@@ -687,15 +656,9 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
             const uint32_t j = e / per_round, r = e - j * per_round;
             const uint32_t b = r / kWaves, w = r - b * kWaves;
             const uint32_t col = g0 + w + j * W;
-            if (col < P.nchunk)
+            if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords)
                 P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
         }
-    } else if (kCount) {
-        const uint32_t k = P.nchunk > gw ? (P.nchunk - gw + W - 1) / W : 0u;   // chunks owned
-        wave_lds_sync();
-        for (uint32_t j = 0; j < k; ++j)
-            for (uint32_t b = lane; b < P.nb; b += kWave)
-                P.seg_cnt[(size_t)b * P.ncol + gw + j * W] = cnt_w[j * P.nb + b];
     }
 }
 
@@ -785,7 +748,7 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
             }
             if (++spins > (1u << 22)) {
                 if (lane == 0)
-                    __hip_atomic_store(P.fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    report_fault(P.fault, YRSS_FAULT_SCAN_TIMEOUT, YRSS_K_SCAN, b, p);
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -807,458 +770,236 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
     reinterpret_cast<uint4 *>(P.off + (size_t)b * P.ncol)[col / 4u] = o;
 }
 
-// q of a scatter round (slot-major: slot j, lane l -> packet r0 + 64 j + l),
-// clamped into the segment so loads never leave it
-__device__ __forceinline__ void load_round(const int16_t *q, uint32_t r0, uint32_t end,
-                                           uint32_t lane, int32_t (&raw)[kScatterRound])
+// ---------------------------------------------------------------------------
+// Kernel 3: stable scatter of packet indices into the per-bucket lists: the
+// FIFO rte_ring_enqueue into dispatch_ring[port][q] of process_packets
+// (ff_dpdk_if.c:1087-1093), for a whole batch.
+//
+// Persistent: as many waves as are resident, wave w taking spans w, w + W, ...
+// (a span is 2^gshift parse chunks, 2048 packets by default), so the waves in
+// flight together cover one stretch of the batch.  A span's lists start at
+// its buckets' prefixes from the scan (start[b] + prefix[b][first chunk]).
+// The span is worked in pieces of up to kPiece packets, each in three steps
+// that touch only LDS and registers:
+//   count  the piece's q (loaded slot-major, 32 x 64 packets, one piece ahead)
+//          is histogrammed per bucket: lanes sharing a bucket are found with
+//          ceil(log2 nb) ballots, the lowest adds the group's size;
+//   place  every packet's stage slot is its bucket's run start + its rank:
+//          the same ballots, and the leader's LDS atomic returns the count
+//          before its group (a wave's LDS atomics run in issue order, so
+//          slots, and therefore the lists, keep packet order);
+//   copy   the stage is written out in order.  A bucket's run starts at a
+//          stage slot congruent to its list position mod 4 (at most 3 words
+//          of padding per bucket), so four stage words that share a bucket
+//          are one aligned 16-byte store; quads in lines the piece writes
+//          whole go out non-temporal, the rest plain (L2 merges a line's
+//          pieces: non-temporal partial lines cost 1.6x,
+//          profiles/r01_v5_scatter_sweep.log).
+// The scatter ranks packets itself from q: the parse kernel only counts per
+// chunk (the scan turns that into the spans' list offsets), and a span's own
+// histogram is checked against those counts at its end.  Any disagreement, and
+// any destination outside the batch, is reported through the fault record
+// instead of stored (YRSS_FAULT_COUNT_MISMATCH / _LIST_RANGE / _STAGE).
+// A batch whose totals show one non-empty list (all-UDP traffic, the headline
+// config) takes the identity path: its list is 0, 1, ..., n-1, written
+// grid-stride as 16-byte non-temporal stores without reading q.
+// ---------------------------------------------------------------------------
+
+// The piece's q (or ranks), slot-major (slot s, lane l -> packet p0 + 64 s +
+// l), one register a slot: packing two slots per register at the load made
+// every pair wait for its loads (and, behind them in the in-order vmcnt
+// queue, for the previous piece's stores).  Lanes past the piece's end read 0
+// through the buffer's range check and are masked by index.
+__device__ __forceinline__ void load_piece(const uint16_t *q, uint32_t p0, uint32_t pe,
+                                           uint32_t lane, uint32_t (&qv)[kPieceSlots])
 {
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(q + p0), 0, (int)((pe - p0) * 2u), kRsrcWord3);
 #pragma unroll
-    for (int j = 0; j < kScatterRound; ++j)
-        raw[j] = __builtin_nontemporal_load(q + min(r0 + j * kWave + lane, end - 1u));
+    for (uint32_t s = 0; s < kPieceSlots; ++s)
+        qv[s] = __builtin_amdgcn_raw_buffer_load_b16(rq, (int)((s * 64u + lane) * 2u), 0,
+                                                     2 /* nt */);
 }
 
-// Segment feeding at most kFewBuckets buckets (the usual case: nb_procs queues
-// plus the default queue).  The bucket list and each bucket's output cursor
-// live in SGPRs for the whole segment.  Per round and listed bucket u, slot j's
-// ballot(bk == u) is an SGPR mask; a lane's destination is cursor(u) + the
-// count of u below it (mbcnt), so ranking costs ~4 VALU per slot per bucket,
-// needs no LDS, and stores go straight from registers.  q of the next round is
-// in flight while a round is ranked.
-__device__ __forceinline__ void scatter_few(const ScatterParams &P, const uint32_t *off,
-                                            const uint32_t *gcnt, uint32_t beg, uint32_t end,
-                                            uint32_t lane, uint32_t *img)
+// Histogram (cnt) or placement (cur, stage) of one piece.  kPlace: each valid
+// packet's stage word is (packet - p0) << 9 | bucket.
+template <bool kPlace>
+__device__ __forceinline__ void rank_piece(const ScatterParams &P,
+                                           const uint32_t (&qv)[kPieceSlots], uint32_t p0,
+                                           uint32_t pe, uint32_t lane_, uint32_t *ctr, uint32_t *stg)
 {
-    uint32_t ub[kFewBuckets], cur[kFewBuckets];
-#pragma unroll
-    for (uint32_t k = 0; k < kFewBuckets; ++k)
-        ub[k] = cur[k] = 0;
-    uint32_t K = 0;
-    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-        const uint32_t b = b0 + lane;
-        uint64_t nz = __ballot(b < P.nb && gcnt[b] != 0);
-        const uint32_t o = b < P.nb ? off[b] : 0u;
-        while (nz) {
-            const uint32_t bit = (uint32_t)__builtin_ctzll(nz);
-            nz &= nz - 1;
-            const uint32_t uu = b0 + bit, oo = __builtin_amdgcn_readlane(o, bit);
-#pragma unroll
-            for (uint32_t k = 0; k < kFewBuckets; ++k)
-                if (k == K) {
-                    ub[k] = uu;
-                    cur[k] = oo;
-                }
-            ++K;
-        }
-    }
-    if (K <= 1) {
-        // The whole segment goes to one list: q need not even be read, and
-        // the list run is beg, beg+1, ... written as 16-byte stores (1 KiB
-        // per wave-instruction) between an unaligned head and tail.
-        const uint32_t len = end - beg, d = cur[0];
-        const uint32_t head = min(len, (4u - (d & 3u)) & 3u);
-        if (lane < head)
-            P.qidx[d + lane] = beg + lane;
-        const uint32_t nv = (len - head) >> 2;
-        u32x4 *dst = reinterpret_cast<u32x4 *>(P.qidx + d + head);
-        for (uint32_t v = lane; v < nv; v += kWave) {
-            const uint32_t x = beg + head + 4u * v;
-            __builtin_nontemporal_store(u32x4{x, x + 1u, x + 2u, x + 3u}, dst + v);
-        }
-        const uint32_t t = head + 4u * nv + lane;
-        if (t < len)
-            P.qidx[d + t] = beg + t;
-        return;
-    }
-    // LDS image (img != null): bucket k's list run [cur0, cur0 + cnt) is
-    // assembled at img[cur + ioff[k]], ioff aligning the run's 128-byte lines
-    // to the image, then leaves as whole lines of 16-byte non-temporal stores.
-    // Plain per-lane stores left the lists' lines dirty in the caches, and
-    // their write-back then ran inside the NEXT batch's parse kernel (+15-17 us
-    // on all-TCP at 2^24 packets, while that kernel's own traffic was at the
-    // probe floor; non-temporal per-lane stores wrote partial lines, 1.6x).
-    uint32_t ioff[kFewBuckets], c0[kFewBuckets];
-    if (img) {
-        uint32_t base = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kFewBuckets; ++k) {
-            c0[k] = cur[k];
-            const uint32_t cnt = k < K ? gcnt[ub[k]] : 0u;
-            ioff[k] = base - (cur[k] & ~(kImgLine - 1u));
-            base += k < K ? (((cur[k] & (kImgLine - 1u)) + cnt + kImgLine - 1u) & ~(kImgLine - 1u))
-                          : 0u;
-        }
-    }
-    constexpr uint32_t kRound = kWave * kScatterRound;
-    int32_t nxt[kScatterRound];
-    load_round(P.q, beg, end, lane, nxt);
-    for (uint32_t r0 = beg; r0 < end; r0 += kRound) {
-        uint32_t bk[kScatterRound];
-        uint64_t vb[kScatterRound];
-#pragma unroll
-        for (int j = 0; j < kScatterRound; ++j) {
-            // pins the use of the prefetched q here, so the compiler cannot
-            // sink it (and the wait for the load) into the previous round
-            asm volatile("" : "+v"(nxt[j]));
-            bk[j] = bucket_of((int16_t)nxt[j], P.nq);
-            vb[j] = __ballot(r0 + j * kWave + lane < end);
-        }
-        if (r0 + kRound < end)
-            load_round(P.q, r0 + kRound, end, lane, nxt);
-        uint32_t dst[kScatterRound];
-#pragma unroll
-        for (int j = 0; j < kScatterRound; ++j)
-            dst[j] = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < kFewBuckets; ++k) {
-            if (k < K) {
-                uint32_t base = cur[k];
-#pragma unroll
-                for (int j = 0; j < kScatterRound; ++j) {
-                    const bool hit = bk[j] == ub[k];
-                    const uint64_t M = __ballot(hit) & vb[j];
-                    const uint32_t r = __builtin_amdgcn_mbcnt_hi(
-                        (uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, base));
-                    dst[j] = hit ? r + (img ? ioff[k] : 0u) : dst[j];
-                    base += (uint32_t)__popcll(M);
-                }
-                cur[k] = base;
-            }
-        }
-        if (img) {
-#pragma unroll
-            for (int j = 0; j < kScatterRound; ++j)
-                if ((vb[j] >> lane) & 1u)
-                    img[dst[j]] = r0 + j * kWave + lane;
-            continue;
-        }
-#pragma unroll
-        for (int j = 0; j < kScatterRound; ++j)
-            if ((vb[j] >> lane) & 1u) {
-                // plain stores: a store covers a few runs, and L2 merges the
-                // partial lines (non-temporal ones cost 1.6x here)
-                P.qidx[dst[j]] = r0 + j * kWave + lane;
-            }
-    }
-    if (!img)
-        return;
-    wave_lds_sync();
-#pragma unroll
-    for (uint32_t k = 0; k < kFewBuckets; ++k) {
-        if (k >= K)
-            break;
-        const uint32_t a = c0[k], e = cur[k];   // this group's run of bucket ub[k]
-        const uint32_t la = (a + kImgLine - 1u) & ~(kImgLine - 1u);
-        const uint32_t le = e & ~(kImgLine - 1u);
-        const uint32_t io = ioff[k];   // image index of global slot g: g + io (mod 2^32)
-        if (la < le) {
-            // whole lines: 16-byte non-temporal stores, 1 KiB per wave-instruction
-            const uint32_t nv = (le - la) >> 2;
-            for (uint32_t v = lane; v < nv; v += kWave) {
-                const uint32_t g = la + 4u * v;
-                const u32x4 x = *reinterpret_cast<const u32x4 *>(img + (g + io));
-                __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(P.qidx + g));
-            }
-            // the partial lines at both ends are shared with the neighbouring
-            // groups' runs: plain 4-byte stores, merged in L2
-            if (lane < la - a)
-                P.qidx[a + lane] = img[a + lane + io];
-            if (lane < e - le)
-                P.qidx[le + lane] = img[le + lane + io];
-        } else {
-            for (uint32_t g = a + lane; g < e; g += kWave)
-                P.qidx[g] = img[g + io];
-        }
-    }
-}
-
-// Image layout of a group's runs (count mode): the runs are packed in bucket
-// order, bucket b's run [off[b], off[b] + gcnt[b]) at image slots
-// [icur[b], icur[b] + gcnt[b]).  The flush works per piece: a global 128-byte
-// line's part inside one run, desc[p] = {image slot - global slot, run start,
-// run end, line}.  Returns the pieces: a run of c slots touches at most
-// (c + 31) / 32 + 1 lines, so at most the group's lines + two per bucket.
-__device__ __forceinline__ uint32_t image_layout(uint32_t nb, const uint32_t *off,
-                                                 const uint32_t *gcnt, uint32_t *icur,
-                                                 u32x4 *desc, uint32_t lane)
-{
-    uint32_t carry = 0, pcarry = 0;
-    for (uint32_t b0 = 0; b0 < nb; b0 += kWave) {
-        const uint32_t b = b0 + lane;
-        const uint32_t cnt = b < nb ? gcnt[b] : 0u, a = b < nb ? off[b] : 0u;
-        const uint32_t L0 = a / kImgLine;
-        const uint32_t np = cnt ? (a + cnt - 1u) / kImgLine - L0 + 1u : 0u;
-        const uint32_t x = wave_incl_scan(cnt, lane), xp = wave_incl_scan(np, lane);
-        const uint32_t ib = carry + x - cnt, pb = pcarry + xp - np;
-        if (b < nb)
-            icur[b] = ib;
-        const u32x4 d = {ib - a, a, a + cnt, 0u};
-        for (uint32_t k = 0; k < np; ++k) {
-            u32x4 e = d;
-            e[3] = L0 + k;
-            desc[pb + k] = e;
-        }
-        carry += __shfl(x, kWave - 1, kWave);
-        pcarry += __shfl(xp, kWave - 1, kWave);
-    }
-    return pcarry;
-}
-
-// Writes a group's image (image_layout) out, a piece per 8 lanes, 16 bytes a
-// lane.  Pieces that are whole lines leave as 16-byte non-temporal stores;
-// the partial lines at a run's ends are shared with the neighbouring groups'
-// runs and go out as plain 4-byte stores, merged in L2.
-__device__ __forceinline__ void flush_image(const ScatterParams &P, const uint32_t *img,
-                                            const u32x4 *desc, uint32_t pieces, uint32_t lane)
-{
-#pragma unroll 2
-    for (uint32_t v = lane; v < pieces * 8u; v += kWave) {
-        const u32x4 d = desc[v / 8u];
-        const uint32_t gl = d[3] * kImgLine, g = gl + 4u * (v & 7u);
-        const uint32_t *src = img + (g + d[0]);
-        if (gl >= d[1] && gl + kImgLine <= d[2]) {
-            const u32x4 x = {src[0], src[1], src[2], src[3]};
-            __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(P.qidx + g));
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < 4u; ++k)
-                if (g + k >= d[1] && g + k < d[2])
-                    P.qidx[g + k] = src[k];
-        }
-    }
-}
-
-// Count mode: the group's q, lane-major (lane l holds packets l*M .. l*M + M-1,
-// M = seg / 64), loaded straight into registers as 16-byte loads first thing
-// in the kernel, so they are in flight while the group's layout is worked
-// out.  Past the batch's end the slots are left 0 (the tail group never reads
-// them, kFull false).
-template <int M>
-__device__ __forceinline__ void count_load(const ScatterParams &P, uint32_t beg, uint32_t end,
-                                           uint32_t lane, u32x4 (&raw)[M / 8])
-{
-    const uint32_t p = beg + lane * (uint32_t)M;
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(P.q + p);
-#pragma unroll
-    for (int i = 0; i < M / 8; ++i) {
-        if (p + 8u * i + 8u <= end) {
-            raw[i] = __builtin_nontemporal_load(src + i);
-        } else {
-            uint32_t h[8];
-#pragma unroll
-            for (uint32_t k = 0; k < 8u; ++k)
-                h[k] = p + 8u * i + k < end ? (uint16_t)P.q[p + 8u * i + k] : 0u;
-            raw[i] = u32x4{h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16,
-                           h[6] | h[7] << 16};
-        }
-    }
-}
-
-// Count mode for groups feeding many buckets: a lane-serial counting sort.
-// A packet's stable rank in its bucket is the bucket's count in lower lanes
-// plus its count among the lane's earlier packets, so there are no ballots,
-// no branches and no counters shared between lanes, and the cost per packet
-// does not depend on the bucket count (the few-bucket path's ranking costs ~5
-// VALU per packet and bucket).  A bucket is min(q as u16, nq) (a negative q is
-// >= 0x8000 as u16, so it lands in the drop bucket nq, as bucket_of), counter
-// cnt[b * 65 + l] is lane l's for bucket b: conflict-free, ~2 VALU per packet
-// to count and ~4 to place.  After the scan over lanes each counter is the
-// lane's next image slot in its bucket.  kFull: the group is whole (else
-// slots past the batch's end are skipped).
-template <int M, bool kFull>
-__device__ __forceinline__ void count_pass(const ScatterParams &P, const u32x4 (&raw)[M / 8],
-                                           uint32_t *mine, uint32_t *img, uint32_t p0,
-                                           uint32_t len, bool place)
-{
-    // 16 packets a batch: their counter bumps go out back to back and the
-    // image stores follow (counters and image are disjoint), so a batch
-    // waits for LDS once rather than once per packet
-    constexpr int kB = 16;
-#pragma unroll
-    for (int e0 = 0; e0 < M; e0 += kB) {
-        uint32_t slot[kB];
-#pragma unroll
-        for (int k = 0; k < kB; ++k) {
-            const uint32_t e = e0 + k;
-            const uint32_t x = raw[e / 8][(e / 2) & 3];
-            const uint32_t b = min((e & 1) ? (x >> 16) : (x & 0xffffu), P.nq);
-            uint32_t *c = mine + b * kCntStride;
-            slot[k] = 0;
-            if (kFull || e < len) {
-                if (place)
-                    slot[k] = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WAVEFRONT);
-                else
-                    __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            }
-        }
-        if (place) {
-#pragma unroll
-            for (int k = 0; k < kB; ++k)
-                if (kFull || (uint32_t)(e0 + k) < len)
-                    img[slot[k]] = p0 + (uint32_t)(e0 + k);
-        }
-    }
-}
-
-template <int M>
-__device__ __forceinline__ void scatter_count(const ScatterParams &P, const u32x4 (&raw)[M / 8],
-                                              const uint32_t *icur, uint32_t *img,
-                                              uint32_t *cnt, uint32_t beg, uint32_t end,
-                                              uint32_t lane)
-{
-    for (uint32_t i = lane; i < P.nb * kCntStride; i += kWave)
-        cnt[i] = 0;
-    wave_lds_sync();
-    uint32_t *mine = cnt + lane;
-    const uint32_t p0 = beg + lane * (uint32_t)M;
-    const uint32_t len = p0 < end ? end - p0 : 0u;   // the lane's packets (M if whole)
-    const bool full = end - beg == (uint32_t)(M * kWave);
-    if (full)
-        count_pass<M, true>(P, raw, mine, img, p0, len, false);
-    else
-        count_pass<M, false>(P, raw, mine, img, p0, len, false);
-    wave_lds_sync();
-    // exclusive scan over lanes, transposed: lane b walks bucket b's 64
-    // counters (stride kCntStride keeps both access patterns conflict-free)
-    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-        const uint32_t b = b0 + lane;
-        if (b < P.nb) {
-            uint32_t run = icur[b];
-            uint32_t *row = cnt + b * kCntStride;
-            for (uint32_t l = 0; l < (uint32_t)kWave; l += 8u) {
-                uint32_t x[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    x[k] = row[l + k];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    row[l + k] = run;
-                    run += x[k];
-                }
-            }
-        }
-    }
-    wave_lds_sync();
-    if (full)
-        count_pass<M, true>(P, raw, mine, img, p0, len, true);
-    else
-        count_pass<M, false>(P, raw, mine, img, p0, len, true);
-}
-
-// General case, any number of buckets, cost independent of nb.  cur[b] in LDS
-// is bucket b's output cursor for this segment.  Per slot, peers (lanes sharing
-// a bucket) come from bit-sliced ballots; the group's lowest lane bumps the
-// cursor with an LDS atomic whose return value is the group's first output
-// slot.  A wave's LDS atomics execute in issue order, so issuing the slots back
-// to back keeps packet order (FIFO) with one wait; the other lanes read their
-// leader's value by ds_bpermute and add their rank inside the group.  Stores
-// go straight from registers.  A full round that is all one bucket (UDP
-// stretches) skips the ballots.
-__device__ __forceinline__ void scatter_general(const ScatterParams &P, uint32_t *cur,
-                                                uint32_t beg, uint32_t end, uint32_t lane)
-{
-    constexpr uint32_t kRound = kWave * kScatterRound;
+    const uint32_t lane = opaque(lane_);
     const uint64_t lt = lane_lt_mask(lane);
-    int32_t nxt[kScatterRound];
-    load_round(P.q, beg, end, lane, nxt);
-    for (uint32_t r0 = beg; r0 < end; r0 += kRound) {
-        uint32_t bk[kScatterRound];
-        uint32_t vmask = 0;
+    constexpr uint32_t kB = 8;   // slots whose LDS atomics issue back to back
 #pragma unroll
-        for (int j = 0; j < kScatterRound; ++j) {
-            asm volatile("" : "+v"(nxt[j]));
-            bk[j] = bucket_of((int16_t)nxt[j], P.nq);
-            vmask |= (r0 + j * kWave + lane < end ? 1u : 0u) << j;
+    for (uint32_t s0 = 0; s0 < kPieceSlots; s0 += kB) {
+        uint32_t bk[kB], first[kB];
+        uint64_t peers[kB];
+        bool valid[kB];
+#pragma unroll
+        for (uint32_t j = 0; j < kB; ++j) {
+            const uint32_t s = s0 + j;
+            const uint32_t p = p0 + s * 64u + lane;
+            valid[j] = p < pe;
+            bk[j] = bucket_of((int16_t)qv[s], P.nq);
+            const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk[j]);
+            if (__all(valid[j] && bk[j] == b0))   // a whole slot of one bucket (UDP stretches)
+                peers[j] = ~0ull;
+            else
+                peers[j] = peer_mask(bk[j], valid[j], P.nb);
         }
-        if (r0 + kRound < end)
-            load_round(P.q, r0 + kRound, end, lane, nxt);
-        const uint32_t B0 = __builtin_amdgcn_readfirstlane(bk[0]);
-        bool same = true;
 #pragma unroll
-        for (int j = 0; j < kScatterRound; ++j)
-            same &= bk[j] == B0;
-        if (end - r0 >= kRound && __all(same)) {
-            const uint32_t base = __builtin_amdgcn_readfirstlane(cur[B0]);
-#pragma unroll
-            for (int j = 0; j < kScatterRound; ++j)
-                P.qidx[base + j * kWave + lane] = r0 + j * kWave + lane;
-            wave_lds_sync();
-            if (lane == 0)
-                cur[B0] = base + kRound;
-            wave_lds_sync();
-            continue;
-        }
-        uint64_t peers[kScatterRound];
-        uint32_t first[kScatterRound];
-#pragma unroll
-        for (int j = 0; j < kScatterRound; ++j)
-            peers[j] = peer_mask(bk[j], (vmask >> j) & 1u, P.nb);
-#pragma unroll
-        for (int j = 0; j < kScatterRound; ++j) {
+        for (uint32_t j = 0; j < kB; ++j) {
             first[j] = 0;
-            if (((vmask >> j) & 1u) && (peers[j] & lt) == 0)
-                first[j] = atomicAdd(&cur[bk[j]], (uint32_t)__popcll(peers[j]));
+            if (valid[j] && (peers[j] & lt) == 0) {
+                if (kPlace)
+                    first[j] = atomicAdd(&ctr[bk[j]], (uint32_t)__popcll(peers[j]));
+                else
+                    atomicAdd(&ctr[bk[j]], (uint32_t)__popcll(peers[j]));
+            }
         }
+        if (kPlace) {
 #pragma unroll
-        for (int j = 0; j < kScatterRound; ++j) {
-            const int leader = peers[j] ? __builtin_ctzll(peers[j]) : (int)lane;
-            const uint32_t dst =
-                __shfl(first[j], leader, kWave) + (uint32_t)__popcll(peers[j] & lt);
-            if ((vmask >> j) & 1u)
-                P.qidx[dst] = r0 + j * kWave + lane;
+            for (uint32_t j = 0; j < kB; ++j) {
+                const int leader = peers[j] ? __builtin_ctzll(peers[j]) : (int)lane;
+                const uint32_t slot =
+                    __shfl(first[j], leader, kWave) + (uint32_t)__popcll(peers[j] & lt);
+                if (valid[j]) {
+                    const uint32_t off = (s0 + j) * 64u + lane;
+                    if (slot < P.stg)
+                        stg[slot] = (off << 9) | bk[j];
+                    else
+                        report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, p0 + off, slot);
+                }
+            }
         }
-        wave_lds_sync();
     }
 }
 
-// ---------------------------------------------------------------------------
-// Kernel 3: stable scatter of packet indices into per-bucket lists.
-// Persistent: as many waves as are resident, wave w taking groups w, w + W,
-// ... (W waves; the waves in flight together cover one stretch of the batch,
-// as a wave per group did).  A wave works out the lists' starts once, and
-// while it works on a group the next group's bucket prefixes (and, in count
-// mode, its q) are already in flight: one wave per group paid those loads'
-// latency once per group (13 us of a 22 us all-TCP scatter at 2^24 packets,
-// 25 us with 65 buckets, where LDS left two waves per CU).
-// M > 0: groups of 64 * M packets feeding more than P.kmin buckets take
-// count mode.
-// ---------------------------------------------------------------------------
-template <int M>
-__global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
+// Writes a piece's stage out, quad by quad: four words of one bucket are one
+// aligned 16-byte store (non-temporal when the piece writes the whole line),
+// others word by word.  Returns how many entries this lane wrote.
+__device__ __forceinline__ uint32_t copy_out(const ScatterParams &P, const uint32_t *stg,
+                                             const uint32_t *base, const uint32_t *ls,
+                                             const uint32_t *cnt, uint32_t p0, uint32_t ph,
+                                             uint32_t lane)
+{
+    uint32_t wrote = 0;
+    for (uint32_t v = lane; v < P.stg / 4u; v += kWave) {
+        const u32x4 e = reinterpret_cast<const u32x4 *>(stg)[v];
+        const uint32_t b = e.x & 511u;
+        if (b < P.nb && (e.y & 511u) == b && (e.z & 511u) == b && (e.w & 511u) == b) {
+            const uint32_t bs = base[b], k0 = 4u * v - ls[b];
+            const uint32_t d = bs + k0;
+            // the quad lies inside its bucket's run, and the run inside the batch
+            if (k0 + 3u < cnt[b] && d + 4u <= P.n && d + 4u > d) {
+                const u32x4 x = {p0 + (e.x >> 9), p0 + (e.y >> 9), p0 + (e.z >> 9),
+                                 p0 + (e.w >> 9)};
+                const uint32_t la = (d + ph) & ~(kImgLine - 1u);   // line, in address units
+                u32x4 *dst = reinterpret_cast<u32x4 *>(P.qidx + d);
+#ifndef YRSS_AB_STORE
+#define YRSS_AB_STORE 0
+#endif
+                if (YRSS_AB_STORE == 1)
+                    *dst = x;
+                else if (YRSS_AB_STORE == 2)
+                    __builtin_nontemporal_store(x, dst);
+                else if (YRSS_AB_STORE == 3)
+                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(x) : "memory");
+                else if (la >= bs + ph && la + kImgLine <= bs + cnt[b] + ph)
+                    __builtin_nontemporal_store(x, dst);
+                else
+                    *dst = x;
+                wrote += 4u;
+            } else {
+                report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, p0 + (e.x >> 9), d);
+            }
+        } else {
+            // a quad across a run boundary or padding: word by word
+            auto one = [&](uint32_t w, uint32_t k) {
+                const uint32_t bk = w & 511u;
+                if (bk >= P.nb)
+                    return;
+                const uint32_t kk = 4u * v + k - ls[bk];
+                const uint32_t d = base[bk] + kk;
+                if (kk < cnt[bk] && d < P.n) {
+                    P.qidx[d] = p0 + (w >> 9);
+                    ++wrote;
+                } else {
+                    report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, p0 + (w >> 9),
+                                 d);
+                }
+            };
+            one(e.x, 0u);
+            one(e.y, 1u);
+            one(e.z, 2u);
+            one(e.w, 3u);
+        }
+    }
+    return wrote;
+}
+
+// A piece's 2048 16-bit words, lane-major: register k of lane l holds words
+// 8 (64 k + l) .. + 7 (four 16-byte loads a lane, the values come packed).
+// The base must be 16-byte aligned; words past pe read 0 (range check).
+__device__ __forceinline__ void load_piece16(const uint16_t *a, uint32_t p0, uint32_t pe,
+                                             uint32_t lane, u32x4 (&v)[kPiece / 512])
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(a + p0), 0, (int)((pe - p0) * 2u), kRsrcWord3);
+    if (((pe - p0) & 7u) == 0) {
+#pragma unroll
+        for (uint32_t k = 0; k < kPiece / 512; ++k)
+            v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 r, (int)((k * 64u + lane) * 16u), 0, 2 /* nt */));
+    } else {
+        // the batch's last piece ends inside a 16-byte vector, which the range
+        // check would drop whole: word by word
+#pragma unroll
+        for (uint32_t k = 0; k < kPiece / 512; ++k) {
+            uint32_t w[4];
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) {
+                const int o = (int)((k * 64u + lane) * 16u + 4u * i);
+                w[i] = __builtin_amdgcn_raw_buffer_load_b16(r, o, 0, 0) |
+                       ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 2, 0, 0) << 16);
+            }
+            v[k] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+    }
+}
+
+// kRanked: the parse kernel wrote each packet's rank in its chunk and a span
+// (one piece) is a whole number of chunks, so a packet's stage slot is
+// off[chunk][bucket] + rank with off from the scan's prefixes: about 13 VALU
+// per 64 packets, where ranking in the scatter (ballot match per slot, twice:
+// histogram then placement) cost ~70 and made the kernel VALU-bound (62-198
+// us against 23-65 at 4-256 buckets, profiles/r03_v1_qrows.log).  !kRanked
+// (chunks longer than a piece: batches past ~2^26 packets with many buckets)
+// ranks in the scatter, piece by piece.
+template <bool kRanked>
+__global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     const uint32_t lane = lane_id();
-    // per wave: start[nb], the lists' starts; off[nb], the group's output
-    // cursor per bucket; gcnt[nb], the group's packet count per bucket;
-    // icur[nb], the image cursors (count mode); the list image; in count mode
-    // the image's line descriptors and the lanes' counters
+    const uint32_t wpb = blockDim.x / kWave;
+    // per wave: start[nb] the lists' starts; base[nb] the piece's first list
+    // slot per bucket; ls[nb] the bucket's run start in the stage; cnt[nb]
+    // the piece's count per bucket; then (ranked) off[chunks][nb], the
+    // placement offsets, or (self-ranked) cur[nb] the placement cursors and
+    // send[nb] the span's end per bucket; then the stage
     uint32_t *start = reinterpret_cast<uint32_t *>(smem) + wave * P.wlds;
-    uint32_t *off = start + P.nb;
-    uint32_t *gcnt = off + P.nb;
-    uint32_t *icur = gcnt + P.nb;
-    uint32_t *img = start + P.aux;
-    const uint32_t W = gridDim.x * (blockDim.x / kWave);
-    const uint32_t gw = xcd_block(P.xcd) * (blockDim.x / kWave) + wave;
+    uint32_t *base = start + P.nb, *ls = base + P.nb, *cnt = ls + P.nb;
+    uint32_t *cur = cnt + P.nb, *send = cur + P.nb;
+    uint32_t *stg = start + P.aux;
+    const uint32_t W = gridDim.x * wpb;
+    const uint32_t gw = xcd_block(P.xcd) * wpb + wave;
     const uint32_t ng = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
-    auto bounds = [&](uint32_t g, uint32_t &beg, uint32_t &end) {
-        beg = g * P.seg;
-        end = P.n - beg > P.seg ? beg + P.seg : P.n;
-    };
-    // a bucket's prefix at chunk column c (its total past the last chunk)
-    auto prefix = [&](uint32_t b, uint32_t c) {
-        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : P.totals[b];
-    };
+    // the lists' 16-byte phase: qidx + d is 16-byte aligned iff (d + ph) % 4 == 0
+    const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 3u);
 
-    u32x4 raw[M > 0 ? M / 8 : 1];
-    if constexpr (M > 0) {
-        if (gw < ng) {
-            uint32_t beg, end;
-            bounds(gw, beg, end);
-            count_load<M>(P, beg, end, lane, raw);
-        }
-    }
-    // list starts (exclusive scan of totals)
+    // list starts (exclusive scan of totals); wave 0 also writes qstart
     uint32_t carry = 0, nzb = 0;
     for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
         const uint32_t b = b0 + lane;
@@ -1267,6 +1008,7 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
         const uint32_t x = wave_incl_scan(t, lane);
         if (b < P.nb) {
             start[b] = carry + x - t;
+            cnt[b] = 0u;
             if (gw == 0)
                 P.qstart[b] = carry + x - t;
         }
@@ -1274,19 +1016,12 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
     }
     if (gw == 0 && lane == 0)
         P.qstart[P.nb] = carry;
-    // buckets 0..63's prefixes for the wave's first group (o: at its first
-    // chunk, oe: at the next group's); more buckets load theirs per group
-    uint32_t o0 = 0, oe0 = 0;
-    if (gw < ng && lane < P.nb) {
-        o0 = prefix(lane, gw << P.gshift);
-        oe0 = prefix(lane, (gw + 1u) << P.gshift);
-    }
-    if (nzb == 1 && P.single) {
-        // the batch feeds one list (all-UDP traffic): it starts at 0 and is
-        // 0, 1, ..., n-1.  Written grid-stride as 16-byte non-temporal stores,
-        // the layout that writes fastest (64 MB in 10.7 us against 11.9 us for
-        // one group per wave, profiles/r02_v8_hbm_write.log); qstart is done.
-        const uint32_t head = min(P.n, (4u - (uint32_t)(((uintptr_t)P.qidx >> 2) & 3u)) & 3u);
+    if (nzb == 1) {
+        // one non-empty list (all-UDP traffic): 0, 1, ..., n-1, grid-stride
+        // 16-byte non-temporal stores, the layout that writes fastest (64 MB
+        // in 10.7 us against 11.9 us for one group per wave,
+        // profiles/r02_v8_hbm_write.log)
+        const uint32_t head = min(P.n, (4u - ph) & 3u);
         const uint32_t nv = (P.n - head) >> 2;
         const uint32_t T = gridDim.x * blockDim.x;
         const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1302,279 +1037,181 @@ __global__ __launch_bounds__(kScatterBlock) void yrss_scatter(ScatterParams P)
             P.qidx[t] = t;
         return;
     }
-    for (uint32_t g = gw; g < ng; g += W) {
-        uint32_t beg, end;
-        bounds(g, beg, end);
-        // this group's cursors and counts, then the next group's prefixes in
-        // flight
-        const bool more = g + W < ng;
-        const uint32_t col = g << P.gshift, col_end = col + (1u << P.gshift);
-        uint32_t kseg = 0;
+    if (gw >= ng)
+        return;
+    auto prefix = [&](uint32_t b, uint32_t c) {
+        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : P.totals[b];
+    };
+    auto span_end = [&](uint32_t g) {
+        const uint64_t e = (uint64_t)g * P.seg + P.seg;
+        return e < P.n ? (uint32_t)e : P.n;
+    };
+    // stage layout from cnt[]: bucket b's run at ls[b] == base[b] + ph (mod 4),
+    // the rest padding (0xFFFFFFFF: bucket field 511 >= nb)
+    auto layout = [&]() {
+        uint32_t raw = 0;
         for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
             const uint32_t b = b0 + lane;
-            uint32_t cnt = 0;
+            const uint32_t w = b < P.nb ? cnt[b] + 3u : 0u;
+            const uint32_t x = wave_incl_scan(w, lane);
             if (b < P.nb) {
-                const uint32_t o = b0 ? prefix(b, col) : o0;
-                cnt = (b0 ? prefix(b, col_end) : oe0) - o;
-                off[b] = start[b] + o;
-                gcnt[b] = cnt;
+                const uint32_t r = raw + x - w;
+                ls[b] = r + ((base[b] + ph - r) & 3u);
             }
-            kseg += (uint32_t)__popcll(__ballot(cnt != 0u));
+            raw += __shfl(x, kWave - 1, kWave);
         }
-        if (more && lane < P.nb) {
-            o0 = prefix(lane, (g + W) << P.gshift);
-            oe0 = prefix(lane, (g + W + 1u) << P.gshift);
-        }
-        wave_lds_sync();
-        if constexpr (M > 0) {
-            if (kseg > P.kmin) {
-                u32x4 *desc = reinterpret_cast<u32x4 *>(img + P.img);
-                const uint32_t words = image_layout(P.nb, off, gcnt, icur, desc, lane);
-                wave_lds_sync();
-                scatter_count<M>(P, raw, icur, img, start + P.cnt_off, beg, end, lane);
-                if (more) {
-                    uint32_t nb0, ne0;
-                    bounds(g + W, nb0, ne0);
-                    count_load<M>(P, nb0, ne0, lane, raw);
-                }
-                wave_lds_sync();
-                flush_image(P, img, desc, words, lane);
-                goto next;
-            }
-            if (more) {
-                uint32_t nb0, ne0;
-                bounds(g + W, nb0, ne0);
-                count_load<M>(P, nb0, ne0, lane, raw);
-            }
-        }
-        if (kseg <= kFewBuckets)
-            scatter_few(P, off, gcnt, beg, end, lane, P.img ? img : nullptr);
-        else
-            scatter_general(P, off, beg, end, lane);
-    next:
-        // the wave's LDS is reused by its next group
-        wave_lds_sync();
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Kernel 3b: scatter with ranks from the parse kernel (many buckets).  Each
-// packet's output slot is start[b] + prefix[b][chunk] + rank: a streaming pass
-// (q and rank read, 2 + 2 B/pkt; index written, 4 B/pkt) whose cost does not
-// depend on the bucket count.  One wave per group of chunks; the chunk's
-// cursors sit in LDS.  Plain stores let L2 merge the scattered 4-byte writes.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kScatterBlock) void yrss_scatter_ranked(ScatterParams P)
-{
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    const uint32_t lane = lane_id();
-    // per wave: start[nb] list starts; cur[nb] the chunk's global cursor per
-    // bucket; lst[nb] the bucket's first slot in the chunk's sorted stage;
-    // stage[chunk] packet index | bucket << ... (two arrays)
-    uint32_t *wbase = reinterpret_cast<uint32_t *>(smem) + wave * P.wlds;
-    uint32_t *start = wbase;
-    uint32_t *cur = start + P.nb;
-    uint32_t *lst = cur + P.nb;
-    uint32_t *sidx = lst + P.nb;
-    uint32_t *sbk = sidx + kRankStage;
-    const uint32_t gw = xcd_block(P.xcd) * (blockDim.x / kWave) + wave;
-
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-        const uint32_t b = b0 + lane;
-        const uint32_t t = b < P.nb ? P.totals[b] : 0u;
-        const uint32_t x = wave_incl_scan(t, lane);
-        if (b < P.nb) {
-            start[b] = carry + x - t;
-            if (gw == 0)
-                P.qstart[b] = carry + x - t;
-        }
-        carry += __shfl(x, kWave - 1, kWave);
-    }
-    if (gw == 0 && lane == 0)
-        P.qstart[P.nb] = carry;
+        for (uint32_t v = lane; v < P.stg / 4u; v += kWave)
+            reinterpret_cast<u32x4 *>(stg)[v] = u32x4{~0u, ~0u, ~0u, ~0u};
+    };
     wave_lds_sync();
 
-    const uint32_t c0 = gw << P.gshift;
-    const uint32_t c1 = min(c0 + (1u << P.gshift), P.nchunk);
-    if (P.img) {
-        // The group's lists are built in a packed LDS image (image_layout)
-        // and leave through flush_image.  A packet's image slot is its
-        // bucket's run start in the image, plus the bucket's packets in the
-        // group's earlier chunks, plus its rank: no stage and no atomics.
-        if (c0 >= c1)
-            return;
-        uint32_t *goff = lst, *gcnt = goff + P.nb, *icur = gcnt + P.nb;
-        uint32_t *img = wbase + P.aux;
-        u32x4 *desc = reinterpret_cast<u32x4 *>(img + P.img);
-        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-            const uint32_t b = b0 + lane;
-            if (b < P.nb) {
-                const uint32_t *row = P.seg_off + (size_t)b * P.ncol;
-                const uint32_t o0 = row[c0], o1 = c1 < P.nchunk ? row[c1] : P.totals[b];
-                goff[b] = start[b] + o0;
-                gcnt[b] = o1 - o0;
+    if constexpr (kRanked) {
+        // tab[b][c], c = 0..nc: the bucket's prefix at the span's chunk c
+        // (c = nc: the next span's first chunk), ncp = 2nc words per bucket;
+        // loaded one span ahead with the q and ranks (kTab words per lane:
+        // layout_for keeps nb x ncp <= 64 kTab), then turned in place into
+        // the placement offsets off[b][c] = ls[b] + the bucket's packets in
+        // the span's chunks before c
+        const uint32_t nc = 1u << P.gshift;   // chunks per span (one piece)
+        const uint32_t lcp = P.gshift + 1u, ntab = P.nb << lcp;
+        uint32_t *tab = cnt + P.nb;
+        u32x4 qp[kPiece / 512], rp[kPiece / 512];
+        uint32_t pt[kTab];
+        auto load_tab = [&](uint32_t g) {
+            const uint32_t c0 = g << P.gshift, ln = opaque(lane);
+#pragma unroll
+            for (uint32_t k = 0; k < kTab; ++k) {
+                const uint32_t e = k * 64u + ln;
+                const uint32_t b = min(e >> lcp, P.nb - 1u), c = min(e & ((2u << P.gshift) - 1u), nc);
+                pt[k] = prefix(b, c0 + c);
             }
-        }
-        wave_lds_sync();
-        const uint32_t pieces = image_layout(P.nb, goff, gcnt, icur, desc, lane);
-        wave_lds_sync();
-        for (uint32_t c = c0; c < c1; ++c) {
-            for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-                const uint32_t b = b0 + lane;
-                if (b < P.nb)   // the run's image start + the bucket's packets before chunk c
-                    cur[b] = icur[b] + start[b] + P.seg_off[(size_t)b * P.ncol + c] - goff[b];
+        };
+        uint32_t g = gw;
+        uint32_t p0 = g * P.seg, pe = span_end(g);
+        load_piece16(reinterpret_cast<const uint16_t *>(P.q), p0, pe, opaque(lane), qp);
+        load_piece16(P.rank, p0, pe, opaque(lane), rp);
+        load_tab(g);
+        for (;;) {
+#pragma unroll
+            for (uint32_t k = 0; k < kTab; ++k)
+                if (k * 64u + lane < ntab)
+                    tab[k * 64u + lane] = pt[k];
+            wave_lds_sync();
+            for (uint32_t b = lane; b < P.nb; b += kWave) {
+                const uint32_t o0 = tab[b << lcp];
+                base[b] = start[b] + o0;
+                cnt[b] = tab[(b << lcp) + nc] - o0;
             }
             wave_lds_sync();
-            const uint32_t pb = c * P.chunk;
-            const uint32_t pe = (uint64_t)pb + P.chunk < P.n ? pb + P.chunk : P.n;
-            for (uint32_t p0 = pb; p0 < pe; p0 += kWave * kScatterRound) {
-                int32_t qv[kScatterRound];
-                uint32_t rv[kScatterRound];
-#pragma unroll
-                for (int j = 0; j < kScatterRound; ++j) {
-                    const uint32_t pc = min(p0 + j * kWave + lane, pe - 1u);
-                    qv[j] = __builtin_nontemporal_load(P.q + pc);
-                    rv[j] = __builtin_nontemporal_load(P.rank + pc);
-                }
-#pragma unroll
-                for (int j = 0; j < kScatterRound; ++j) {
-                    const uint32_t p = p0 + j * kWave + lane;
-                    if (p < pe)
-                        img[cur[bucket_of((int16_t)qv[j], P.nq)] + rv[j]] = p;
-                }
+            layout();
+            wave_lds_sync();
+            for (uint32_t b = lane; b < P.nb; b += kWave) {
+                uint32_t *t = tab + (b << lcp);
+                const uint32_t l = ls[b], o0 = t[0];
+                for (uint32_t c = 0; c < nc; ++c)
+                    t[c] = l + t[c] - o0;
             }
             wave_lds_sync();
-        }
-        flush_image(P, img, desc, pieces, lane);
-        return;
-    }
-    if (P.gstage) {
-        // One counting-sort stage for the whole group, entries packed as
-        // (packet - group start) << 9 | bucket: a bucket's run is all its
-        // packets of the group, so each 64-lane store of the copy-out covers
-        // a few long runs instead of one short run per bucket and chunk.
-        // Stage slot = lst[b] + (prefix[b][c] - prefix[b][c0]) + rank.
-        if (c0 >= c1)
-            return;
-        uint32_t *gcur = cur, *coff = lst + P.nb;
-        uint32_t *stg = coff + P.nb;
-        uint32_t ls = 0;
-        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-            const uint32_t b = b0 + lane;
-            uint32_t o = 0, cnt = 0;
-            if (b < P.nb) {
-                const uint32_t *row = P.seg_off + (size_t)b * P.ncol;
-                o = row[c0];
-                cnt = (c1 < P.nchunk ? row[c1] : P.totals[b]) - o;
+            // place: stage slot = off[bucket][chunk] + rank, entry (packet -
+            // p0) << 9 | bucket; lanes past the span's end store into the
+            // spare word after the stage.  No branch per slot: the copy-out
+            // checks every entry against its bucket's run and counts them.
+            // packet o = 8 (64 k + lane) + j; chunks are multiples of 8
+            // packets, so its chunk is (512 k + 8 lane) >> cshift for every j
+            const uint32_t len = pe - p0, ln = opaque(lane);
+#pragma unroll
+            for (uint32_t k = 0; k < kPiece / 512; ++k) {
+                const uint32_t o8 = (k * 64u + ln) * 8u;
+                const uint32_t *tk = tab + (o8 >> P.cshift);
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j) {
+                    const uint32_t w = j >> 1, sh = 16u * (j & 1u);
+                    const uint32_t b = bucket_of((int16_t)((qp[k][w] >> sh) & 0xffffu), P.nq);
+                    const uint32_t r = (rp[k][w] >> sh) & 0xffffu;
+                    const uint32_t slot = min(tk[b << lcp] + r, P.stg);
+                    stg[o8 + j < len ? slot : P.stg] = ((o8 + j) << 9) | b;
+                }
             }
-            const uint32_t x = wave_incl_scan(cnt, lane);
-            if (b < P.nb) {
-                gcur[b] = start[b] + o;
-                lst[b] = ls + x - cnt;
-            }
-            ls += __shfl(x, kWave - 1, kWave);
-        }
-        wave_lds_sync();
-        const uint32_t gb = c0 * P.chunk;
-        for (uint32_t c = c0; c < c1; ++c) {
-            for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-                const uint32_t b = b0 + lane;
-                if (b < P.nb)
-                    coff[b] = lst[b] + P.seg_off[(size_t)b * P.ncol + c] + start[b] - gcur[b];
+            // the next span's q, ranks and prefixes are in flight during the
+            // copy-out
+            const uint32_t g2 = g + W;
+            const bool more = g2 < ng;
+            const uint32_t p2 = more ? g2 * P.seg : 0u, pe2 = more ? span_end(g2) : 0u;
+            if (more) {
+                load_piece16(reinterpret_cast<const uint16_t *>(P.q), p2, pe2, opaque(lane), qp);
+                load_piece16(P.rank, p2, pe2, opaque(lane), rp);
+                load_tab(g2);
             }
             wave_lds_sync();
-            const uint32_t pb = c * P.chunk;
-            const uint32_t pe = (uint64_t)pb + P.chunk < P.n ? pb + P.chunk : P.n;
-            for (uint32_t p0 = pb; p0 < pe; p0 += kWave * kScatterRound) {
-                int32_t qv[kScatterRound];
-                uint32_t rv[kScatterRound];
-#pragma unroll
-                for (int j = 0; j < kScatterRound; ++j) {
-                    const uint32_t pc = min(p0 + j * kWave + lane, pe - 1u);
-                    qv[j] = P.q[pc];
-                    rv[j] = P.rank[pc];
+            uint32_t wrote = copy_out(P, stg, base, ls, cnt, p0, ph, lane);
+            // every packet of the span left exactly once: two packets on one
+            // slot would leave a hole (padding) inside a run
+            wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
+            if (lane == 0 && wrote != pe - p0)
+                report_fault(P.fault, YRSS_FAULT_COUNT_MISMATCH, YRSS_K_SCATTER, g, wrote);
+            wave_lds_sync();
+            if (!more)
+                break;
+            g = g2;
+            p0 = p2;
+            pe = pe2;
+        }
+    } else {
+        uint32_t g = gw, p0 = gw * P.seg;
+        uint32_t pe = min(span_end(g), p0 + kPiece);
+        uint32_t qv[kPieceSlots], qn[kPieceSlots];
+        load_piece(reinterpret_cast<const uint16_t *>(P.q), p0, pe, opaque(lane), qv);
+        for (;;) {
+            const uint32_t se = span_end(g);
+            if (p0 == g * P.seg) {
+                // a new span: its lists' first slots and, for the check at its
+                // end, where each bucket's run must finish
+                const uint32_t c0 = g << P.gshift, c1 = c0 + (1u << P.gshift);
+                for (uint32_t b = lane; b < P.nb; b += kWave) {
+                    base[b] = start[b] + prefix(b, c0);
+                    send[b] = start[b] + prefix(b, c1);
                 }
-#pragma unroll
-                for (int j = 0; j < kScatterRound; ++j) {
-                    const uint32_t p = p0 + j * kWave + lane;
-                    if (p < pe) {
-                        const uint32_t b = bucket_of((int16_t)qv[j], P.nq);
-                        const uint32_t slot = coff[b] + rv[j];
-                        if (slot < P.seg)   // guard: counts and ranks always agree
-                            stg[slot] = ((p - gb) << 9) | b;
-                        else if (P.fault)   // reported as -EIO (yrss_status), never a fault
-                            __hip_atomic_store(P.fault, 2u, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
-                }
+                wave_lds_sync();
+            }
+            // count
+            rank_piece<false>(P, qv, p0, pe, lane, cnt, stg);
+            wave_lds_sync();
+            layout();
+            for (uint32_t b = lane; b < P.nb; b += kWave)
+                cur[b] = ls[b];
+            wave_lds_sync();
+            // place
+            rank_piece<true>(P, qv, p0, pe, lane, cur, stg);
+            // the next piece's q is in flight during the copy-out
+            uint32_t g2 = g, p2 = pe;
+            if (pe >= se) {
+                g2 = g + W;
+                p2 = g2 * P.seg;
+            }
+            const bool more = g2 < ng;
+            const uint32_t pe2 = more ? min(span_end(g2), p2 + kPiece) : 0u;
+            if (more)
+                load_piece(reinterpret_cast<const uint16_t *>(P.q), p2, pe2, opaque(lane), qn);
+            wave_lds_sync();
+            (void)copy_out(P, stg, base, ls, cnt, p0, ph, lane);
+            wave_lds_sync();
+            // the next piece's lists start where this one's end
+            for (uint32_t b = lane; b < P.nb; b += kWave) {
+                base[b] += cnt[b];
+                cnt[b] = 0u;
+                if (pe >= se && base[b] != send[b])
+                    report_fault(P.fault, YRSS_FAULT_COUNT_MISMATCH, YRSS_K_SCATTER, g, b);
             }
             wave_lds_sync();
-        }
-        const uint32_t ge = (uint64_t)c1 * P.chunk < P.n ? c1 * P.chunk : P.n;
-        for (uint32_t k = lane; k < ge - gb; k += kWave) {
-            const uint32_t e = stg[k], b = e & 511u;
-            const uint32_t d = b < P.nb ? gcur[b] + (k - lst[b]) : P.n;
-            if (d < P.n)   // guard: a stage slot left unwritten never faults
-                P.qidx[d] = gb + (e >> 9);
-            else if (P.fault)
-                __hip_atomic_store(P.fault, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        return;
-    }
-    for (uint32_t c = c0; c < c1; ++c) {
-        // the chunk's cursor per bucket and its counting-sort layout: bucket b
-        // holds stage slots [lst[b], lst[b] + count), count from the prefix
-        // difference to the next chunk
-        uint32_t ls = 0;
-        for (uint32_t b0 = 0; b0 < P.nb; b0 += kWave) {
-            const uint32_t b = b0 + lane;
-            uint32_t o = 0, cnt = 0;
-            if (b < P.nb) {
-                const uint32_t *row = P.seg_off + (size_t)b * P.ncol;
-                o = row[c];
-                cnt = (c + 1 < P.nchunk ? row[c + 1] : P.totals[b]) - o;
-            }
-            const uint32_t x = wave_incl_scan(cnt, lane);
-            if (b < P.nb) {
-                cur[b] = start[b] + o;
-                lst[b] = ls + x - cnt;
-            }
-            ls += __shfl(x, kWave - 1, kWave);
-        }
-        wave_lds_sync();
-        const uint32_t pb = c * P.chunk;
-        const uint32_t pe = (uint64_t)pb + P.chunk < P.n ? pb + P.chunk : P.n;
-        // place: slot lst[b] + rank
-        for (uint32_t p0 = pb; p0 < pe; p0 += kWave * kScatterRound) {
-            int32_t qv[kScatterRound];
-            uint32_t rv[kScatterRound];
+            if (!more)
+                break;
+            g = g2;
+            p0 = p2;
+            pe = pe2;
 #pragma unroll
-            for (int j = 0; j < kScatterRound; ++j) {
-                const uint32_t pc = min(p0 + j * kWave + lane, pe - 1u);
-                qv[j] = P.q[pc];
-                rv[j] = P.rank[pc];
-            }
-#pragma unroll
-            for (int j = 0; j < kScatterRound; ++j) {
-                const uint32_t p = p0 + j * kWave + lane;
-                if (p < pe) {
-                    const uint32_t b = bucket_of((int16_t)qv[j], P.nq);
-                    const uint32_t k = lst[b] + rv[j];
-                    sidx[k] = p;
-                    sbk[k] = b;
-                }
-            }
+            for (uint32_t k = 0; k < kPieceSlots; ++k)
+                qv[k] = qn[k];
         }
-        wave_lds_sync();
-        // copy out: a bucket's packets are consecutive in the stage and in
-        // its list, so stores form runs of chunk/nb entries
-        for (uint32_t k = lane; k < pe - pb; k += kWave) {
-            const uint32_t b = sbk[k];
-            P.qidx[cur[b] + (k - lst[b])] = sidx[k];
-        }
-        wave_lds_sync();
     }
 }
 
@@ -2001,13 +1638,17 @@ __device__ void small_burst_body(const ParseParams &P, const GatherParams &G, co
         const uint32_t t = wave + j * kSmallWaves;
         if (t >= ntiles)
             break;
-        flush_out<kFilter, false>(P, L.oq + j * kTile, L.oh + j * kTile, L.of + j * kTile,
-                                  L.orank + j * kTile, t * kTile, 1u, lane);
+        flush_out<kFilter>(P, L.oq + j * kTile, L.oh + j * kTile, L.of + j * kTile,
+                           L.orank + j * kTile, t * kTile, 1u, lane);
         const uint32_t pkt = t * kTile + lane;
         if (pkt < P.n) {
             if (S.qidx) {
                 const uint32_t b = bucket_of((int16_t)L.oq[j * kTile + lane], P.nq);
-                S.qidx[L.start[b] + L.cnt[t * P.nb + b] + L.orank[j * kTile + lane]] = pkt;
+                const uint32_t d = L.start[b] + L.cnt[t * P.nb + b] + L.orank[j * kTile + lane];
+                if (d < P.n)
+                    S.qidx[d] = pkt;
+                else
+                    report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_BURST, pkt, d);
             }
             if (S.writeback) {
                 const uint64_t m = gio.ptrs[pkt];
@@ -2237,8 +1878,8 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         P.q = static_cast<int16_t *>(out_ptr(0));
         P.hash = static_cast<uint32_t *>(out_ptr(1));
         P.filter = nullptr;
-        P.rank = nullptr;
         P.seg_cnt = nullptr;
+        P.rank = nullptr;
         P.out16 = 0;
         const uint32_t frames = (ctl[2] & kWorkerFrames) ? 1u : 0u;
         const GatherIO gio{W.ptrs + (size_t)si * kWorkerMaxBurst,
@@ -2337,7 +1978,7 @@ struct PendingBurst {
     uint32_t n = 0;
     HostOut outs[5] = {};            // q, hash, qidx, qstart, filter
     bool gather_fault = false;       // zero-copy: a pointer outside every range
-    bool scan_fault = false;         // multi-kernel path: scan look-back fault
+    bool dev_fault = false;          // multi-kernel path: check the fault record
     uint64_t done_seq = 0;           // one-launch path: value the kernel stores in *h_done
     void *const *wb_mbufs = nullptr; // host-side hash.rss write-back (staged path)
 };
@@ -2346,15 +1987,11 @@ struct yrss_ctx {
     yrss_config cfg;
     int device = 0;
     int cus = 0;
-    // Parse-kernel launch shape (env overrides for tuning sweeps).  Defaults =
-    // best of the on-hardware sweeps (profiles/r01_sweep_*.json,
-    // r01_v30_occupancy_ab.log): non-temporal window loads are worth ~25 %; one
-    // 512-thread workgroup (8 waves) per CU beats 12 or 16 resident waves.
-    uint32_t parse_block = 512;  // YRSS_BLOCK: 256 / 512
-    bool nt = true;              // YRSS_NT
-    uint32_t waves_per_cu = 8;   // YRSS_WAVES_PER_CU: cap on resident waves
-    uint32_t lds_blocks = 0;     // YRSS_LDS_BLOCKS: blocks per CU by LDS (0 = sized for the filter)
-    unsigned event_flags = hipEventDisableSystemFence;   // YRSS_EVENT_FLAGS
+    // Parse-kernel launch shape: one 512-thread workgroup (8 waves) per CU,
+    // the best of the on-hardware sweeps (profiles/r01_sweep_*.json,
+    // r01_v30_occupancy_ab.log: 12 resident waves were equal, 16 worse).
+    // yrss_set_tuning overrides the layout for tests and measurements.
+    yrss_tuning tune{};
     uint32_t nb = 0;
     ParseParams proto{};         // key schedule, modulo constants
     // KNI (protocol_filter) state, ff_dpdk_kni.c:60-61 / ff_dpdk_if.c:103-104
@@ -2362,32 +1999,15 @@ struct yrss_ctx {
     bool kni_accept = false;
     uint8_t kni_bm[2 * 8192] = {};   // tcp bitmap then udp bitmap, htons-indexed
     uint32_t *d_kni = nullptr;
-    // compaction workspace, sized for the largest grid
-    uint32_t seg_cap = 0;
-    uint32_t chunk_tiles = 0;       // 0: by bucket count (layout_for())
-    uint32_t group_tiles = 0;       // 0: 64
-    uint16_t *d_rank = nullptr;     // ranked mode workspace (n x u16), grown on demand
-    bool no_rank = false;           // YRSS_NO_RANK: ballot scatter even for many buckets
-    bool no_img = false;            // YRSS_NO_IMG: few-bucket lists stored per lane, not via LDS
-    bool no_single = false;         // YRSS_NO_SINGLE: no grid-stride path for one-list batches
-    bool no_count = false;          // YRSS_NO_COUNT: no count-mode scatter
-    bool scatter_full = false;      // YRSS_SCATTER_FULL: a scatter wave per group
-    int rank_img = -1;              // YRSS_RANK_IMG: ranked scatter through an LDS image
-                                    // (1 on, 0 off, -1 up to kRankImgMaxNb[Rr] buckets)
     struct Occ {
         const void *fn;
         uint32_t block, lds, blocks;
     };
     std::vector<Occ> occ;           // resident_blocks cache
-    uint32_t count_kmin = kFewBuckets;   // YRSS_COUNT_KMIN: count mode above this many buckets
-    uint32_t count_max_nb = 9;      // YRSS_COUNT_MAXNB: count mode up to this many buckets (off)
-    uint32_t scatter_wpb = 0;       // YRSS_SCATTER_WPB: waves per scatter workgroup (0: auto)
-    int scatter_xcd = -1;           // YRSS_SCATTER_XCD: XCD-contiguous scatter groups (-1: auto)
-    bool rank_gstage = true;        // YRSS_RANK_GSTAGE: ranked stage per group, packed entries
-    uint32_t rank_min_nb = 7;       // YRSS_RANK_MINNB: ranked scatter past this many buckets
+    uint16_t *d_rank = nullptr;     // ranked scatter workspace (n x u16), grown on demand
     size_t rank_cap = 0;
     unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
-    uint32_t *d_scan_fault = nullptr;   // host-coherent pinned word (yrss_status)
+    uint32_t *d_fault_rec = nullptr;    // host-coherent fault record {code, kernel, where, value}
     uint32_t scan_epoch = 0;
     uint32_t *d_seg_cnt = nullptr;
     uint32_t *d_seg_off = nullptr;
@@ -2420,11 +2040,8 @@ struct yrss_ctx {
     uint64_t *h_done = nullptr;     // host-coherent completion word of yrss_burst_small
     uint64_t *dh_done = nullptr;
     uint64_t done_seq = 0;
-    bool spin_wait = true;          // YRSS_SPIN_WAIT=0: always hipStreamSynchronize
     // device views of the pinned staging: the small-burst kernel reads and
     // writes it in place (no copies)
-    bool no_small = false;          // YRSS_NO_SMALL: always the multi-kernel path
-    bool small_dev = true;          // YRSS_SMALL_DEV=0: device batches never take it
     uint8_t *dh_win = nullptr;
     uint16_t *dh_len = nullptr;
     int16_t *dh_q = nullptr;
@@ -2500,180 +2117,92 @@ int hip_fail(const char *what, hipError_t e)
             return hip_fail(#call, e_);                  \
     } while (0)
 
-size_t parse_lds(const yrss_ctx *c, bool filter)
+constexpr uint32_t kParseBlock = 512;   // 8 waves: one workgroup per CU (LDS)
+
+size_t parse_lds(bool filter)
 {
-    const size_t w = c->parse_block / kWave;
+    constexpr size_t w = kParseBlock / kWave;
     return kTblBytes + w * kStageBytes + w * (kCntWords * sizeof(uint32_t) + kOutBytes) +
            (filter ? kKniWords * sizeof(uint32_t) : 0u);
 }
 
-// The grid does not depend on whether the filter is on, so a segment layout
+// One workgroup per CU (the LDS of the filter variant admits no second), so
+// the grid does not depend on whether the filter is on and a batch's layout
 // (and its compaction) is the same for every variant.
 uint32_t grid_for(const yrss_ctx *c, uint32_t n)
 {
-    const uint32_t wpb = c->parse_block / kWave;
-    const uint64_t per_block = (uint64_t)wpb * kTile;
+    const uint64_t per_block = (uint64_t)(kParseBlock / kWave) * kTile;
     const uint32_t want = (uint32_t)(((uint64_t)n + per_block - 1) / per_block);
-    const uint32_t by_lds =
-        c->lds_blocks ? c->lds_blocks : (uint32_t)(160u * 1024u / parse_lds(c, true));
-    const uint32_t by_waves = std::max(1u, c->waves_per_cu / wpb);
-    const uint32_t cap = (uint32_t)c->cus * std::max(1u, std::min(by_lds, by_waves));
+    const uint32_t cap = c->tune.parse_blocks ? c->tune.parse_blocks : (uint32_t)c->cus;
     return std::max(1u, std::min(want, cap));
 }
 
 // Work layout of one launch.
-// - chunk (ct tiles): the unit the parse kernel deals round-robin to its waves
-//   and counts per bucket.  Small chunks keep the chip's reads in a compact
-//   window; each wave keeps one LDS count slot per chunk it owns, so
-//   chunks <= waves x (kCntWords / nb), and more buckets get larger chunks.
-// - group (2^shift chunks, >= 64 tiles): one scatter wave.
+// - chunk (2^ct_shift tiles): the unit the parse kernel deals round-robin to
+//   its waves and counts per bucket.  Small chunks keep the chip's reads in a
+//   compact window; each wave keeps one LDS count slot (nb words) per chunk it
+//   owns, so chunks <= waves x (kCntWords / nb): 4 tiles up to 64 buckets at
+//   2^24 packets, larger past that or past 2^24 packets.
+// - span (2^shift chunks, 32 tiles = 2048 packets by default): one scatter
+//   wave's unit, worked in pieces of kPiece packets.
 // - ncol: chunk columns rounded up to whole scan tiles.
 struct Layout {
-    uint32_t chunk, ct_shift, shift, seg, nchunk, ncol, nseg;
+    uint32_t chunk, ct_shift, shift, seg, nchunk, ncol;
 };
 
 Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
 {
-    const uint64_t waves = (uint64_t)grid * (c->parse_block / kWave);
+    const uint64_t waves = (uint64_t)grid * (kParseBlock / kWave);
     const uint64_t slots = std::max<uint32_t>(1u, kCntWords / c->nb);
     const uint64_t max_chunks = std::min<uint64_t>(kMaxChunks, waves * slots);
     const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
-    // 4 tiles up to 17 buckets, else 16 (1024 packets, the ranked path's
-    // stage); larger when the waves' count slots run out (at 2^24 packets
-    // from 257 buckets: 2048 slot words per wave, profiles/r02_v11_count_sweep.log)
-    uint64_t ct = c->chunk_tiles ? c->chunk_tiles : (c->nb <= 17u ? 4u : 16u);
-    ct = std::max<uint64_t>(ct, (tiles + max_chunks - 1) / max_chunks);
+    // the ranked scatter keeps 2 x (span chunks) prefixes per bucket (at most
+    // 64 kTab words a wave): 4-tile chunks up to 64 buckets, 8 to 128, 16 to
+    // 256, 32 (one chunk a span) past that
+    const uint64_t ct_nb = c->nb <= 64u ? 4u : c->nb <= 128u ? 8u : c->nb <= 256u ? 16u : 32u;
+    uint64_t ct = std::max<uint64_t>(c->tune.chunk_tiles ? c->tune.chunk_tiles : ct_nb,
+                                     (tiles + max_chunks - 1) / max_chunks);
     uint32_t ct_shift = 0;
     while ((1ull << ct_shift) < ct)
         ++ct_shift;
     ct = 1ull << ct_shift;
-    // scatter groups: 2048 packets for the few-bucket LDS image path (nb <=
-    // 8: a 9-10 KB image per wave, 3-4 workgroups per CU; 4096 had half the
-    // occupancy, 1024 left more partial list lines dirty:
-    // profiles/r02_v10_group_ab.log), count mode (10..25 buckets) and past
-    // 65 buckets; 4096 for the ranked path at 26..65 buckets
-    // (r01_v5_scatter_sweep.log, profiles/r02_v11_count_sweep.log)
-    const uint64_t gt = c->group_tiles ? c->group_tiles
-                                       : (c->nb <= c->count_max_nb || c->nb > 65u || c->rank_gstage
-                                              ? 32u : 64u);
+    const uint64_t st = c->tune.span_tiles ? c->tune.span_tiles : kPiece / kTile;
     Layout L;
     L.ct_shift = ct_shift;
     L.shift = 0;
-    while ((ct << L.shift) < gt)
+    while ((ct << L.shift) < st)
         ++L.shift;
     L.chunk = (uint32_t)(ct * kTile);
     L.seg = L.chunk << L.shift;
     L.nchunk = (uint32_t)(((uint64_t)n + L.chunk - 1) / L.chunk);
     L.ncol = (L.nchunk + kScanTile - 1) / kScanTile * kScanTile;
-    // whole scatter workgroups
-    L.nseg = (uint32_t)((((uint64_t)n + L.seg - 1) / L.seg + kScatterWaves - 1) /
-                        kScatterWaves * kScatterWaves);
     return L;
 }
 
-// LDS of one scatter wave: its cursors (aux words), the group's list image
-// (img words, 0 = none) and, in count mode (cnt_off != 0), the image's piece
-// descriptors and the lanes' counters; wpb waves per workgroup, halved until
-// a workgroup holds at most 64 KiB.  m: count mode's packets per lane (0 =
-// off).  The image holds a few-bucket group's runs with two lines of slack
-// per bucket (few_img), which also holds a count-mode group's packed runs.
+// LDS of one scatter wave: the per-bucket arrays (aux words: four, plus the
+// placement offsets of every chunk of a span when ranked, two more when
+// self-ranked) and the stage (a piece plus up to 3 words of alignment padding
+// per bucket); wpb waves per workgroup, halved until a workgroup holds at most
+// 64 KiB.  ranked: the parse kernel's ranks place packets; it needs a span of
+// at most one piece and its offset table in the wave's share.
 struct ScatterLds {
-    uint32_t aux, img, wlds, wpb, cnt_off, m;
-    uint32_t gstage = 0;   // ranked: one packed stage per group
+    uint32_t aux, stg, wlds, wpb;
+    bool ranked;
 };
 constexpr uint32_t kScatterLdsMax = 64u * 1024u / 4u;   // words per workgroup
 
-// the few-bucket path's image: the group plus two lines of slack per bucket
-uint32_t few_img(const Layout &lay, uint32_t nb)
+ScatterLds scatter_lds(uint32_t nb, const Layout &lay)
 {
-    return lay.seg + 2u * kImgLine * std::min(nb, kFewBuckets);
-}
-
-// XCD-contiguous scatter groups from 10 buckets (count mode and the ranked
-// paths): the L2 merges the run-boundary lines that neighbouring groups
-// share, so fewer partial lines are written back, most of them inside the
-// next parse kernel.  All-TCP step on one box: +3 % at 17 buckets, +2 % at
-// 33, -1 % at 65, +1 % at 129, +5 % at 256; the few-bucket path (9 buckets)
-// lost 1.5 %, UDP/TCP at 4 buckets even (profiles/r02_v15_xcd_ab.log).
-bool scatter_xcd_on(const yrss_ctx *c)
-{
-    return c->scatter_xcd >= 0 ? c->scatter_xcd != 0 : c->nb >= 10u;
-}
-
-void scatter_wpb(const yrss_ctx *c, ScatterLds &r)
-{
-    r.wpb = c->scatter_wpb ? c->scatter_wpb : (uint32_t)kScatterWaves;
+    ScatterLds r;
+    const uint32_t nc = 1u << lay.shift;
+    r.stg = (kPiece + 3u * nb + 3u) & ~3u;
+    r.ranked = lay.seg <= kPiece && nb * 2u * nc <= kTab * kWave &&
+               (4u + 2u * nc) * nb + r.stg + 4u <= kScatterLdsMax;
+    r.aux = ((r.ranked ? 4u + 2u * nc : 6u) * nb + 3u) & ~3u;
+    r.wlds = r.aux + r.stg + 4u;   // + the ranked placement's spare word
+    r.wpb = (uint32_t)kScatterWaves;
     while (r.wpb > 1 && r.wpb * r.wlds > kScatterLdsMax)
         r.wpb /= 2;
-}
-
-// Count mode: for 10..count_max_nb buckets, off by default since the ranked
-// path's group stage: that was +5-7 % at 21 buckets
-// (profiles/r02_v26_gstage2_ab.log) and +0.5-3 % at 13 and 17
-// (profiles/r02_v27_gstage3_ab.log); before it count mode held 10..25
-// (profiles/r02_v11_count_sweep.log).  With 9 buckets the groups rarely feed
-// more than 8 (nb_procs 8 with dispatch_only_core hashes to 7 queues), and
-// count mode's larger LDS share and unused q loads cost the few-bucket path
-// 8 %.  It needs 32 or 64 packets per lane and its image and counters within
-// one wave's LDS share.
-ScatterLds count_lds(const yrss_ctx *c, const Layout &lay)
-{
-    ScatterLds r{};
-    const uint32_t nb = c->nb;
-    if (c->no_img || c->no_count || nb <= c->count_kmin + 1u || nb > c->count_max_nb ||
-        (lay.seg != 2048u && lay.seg != 4096u))
-        return r;
-    r.m = lay.seg / kWave;
-    r.aux = (4u * nb + 3u) & ~3u;
-    r.img = few_img(lay, nb);   // also the few-bucket groups' image (>= the packed runs)
-    r.cnt_off = r.aux + r.img + (lay.seg / kImgLine + 2u * nb) * 4u;   // image_layout's pieces
-    r.wlds = (r.cnt_off + kCntStride * nb + 3u) & ~3u;
-    if (r.wlds > kScatterLdsMax)
-        return ScatterLds{};
-    scatter_wpb(c, r);
-    return r;
-}
-
-ScatterLds scatter_lds(const yrss_ctx *c, const Layout &lay, bool ranked)
-{
-    const uint32_t nb = c->nb;
-    ScatterLds r{};
-    if (ranked) {
-        // By default one packed counting-sort stage per 2048-packet group
-        // (gstage): all-TCP step against the best earlier path, same box,
-        // +5-7 % at 21 buckets (count mode), +6-7 % at 26-33 (LDS image),
-        // +11-15 % at 41-65 (LDS image), +7.5 % at 129 and +6 % at 256
-        // (per-chunk stage): profiles/r02_v25_gstage_ab.log,
-        // r02_v26_gstage2_ab.log.  With it off: the packed image (its pieces
-        // go out a line part per 8 lanes), which gained up to 33 buckets
-        // (profiles/r02_v11_count_sweep.log; 65 with XCD-contiguous groups),
-        // else the per-chunk stage.
-        r.aux = (6u * nb + 3u) & ~3u;
-        r.img = lay.seg;
-        const uint32_t w = r.aux + r.img + (lay.seg / kImgLine + 2u * nb) * 4u;
-        // With XCD-contiguous groups the image pays up to 65 buckets (all-TCP
-        // step +2..6 % at 49, +0.5..2 % at 65; -4 % at 129, -13 % at 256:
-        // profiles/r02_v16_rankimg_xcd_ab.log); round-robin, up to 33.
-        const uint32_t img_max = scatter_xcd_on(c) ? kRankImgMaxNb : kRankImgMaxNbRr;
-        const bool on = c->rank_img < 0 ? !c->rank_gstage && nb <= img_max : c->rank_img > 0;
-        if (on && !c->no_img && w <= kScatterLdsMax) {
-            r.wlds = w;
-        } else if (c->rank_gstage && lay.seg <= 4096u && nb <= 512u &&
-                   4u * nb + lay.seg <= kScatterLdsMax) {
-            r.aux = r.img = 0;
-            r.gstage = 1;
-            r.wlds = (4u * nb + lay.seg + 3u) & ~3u;
-        } else {
-            r.aux = r.img = 0;
-            r.wlds = 3u * nb + 2u * kRankStage;
-        }
-    } else {
-        r.aux = (4u * nb + 3u) & ~3u;
-        if (!c->no_img && lay.seg <= kImgPkts)
-            r.img = few_img(lay, nb);
-        r.wlds = r.aux + r.img;
-    }
-    scatter_wpb(c, r);
     return r;
 }
 
@@ -2695,27 +2224,16 @@ uint32_t resident_blocks(yrss_ctx *c, const void *fn, uint32_t block, uint32_t l
 
 typedef void (*ParseKernel)(ParseParams);
 
-template <int C, bool F, bool NT>
-ParseKernel pick_block(uint32_t block)
-{
-    return block == 256 ? yrss_parse_hash<C, F, NT, 256> : yrss_parse_hash<C, F, NT, 512>;
-}
-
-template <int C>
-ParseKernel pick_fn(const yrss_ctx *c, bool filter)
+// count: 0 none, 1 per-chunk counts, 2 counts + per-packet chunk ranks
+ParseKernel pick_parse(int count, bool filter)
 {
     if (filter)
-        return c->nt ? pick_block<C, true, true>(c->parse_block)
-                     : pick_block<C, true, false>(c->parse_block);
-    return c->nt ? pick_block<C, false, true>(c->parse_block)
-                 : pick_block<C, false, false>(c->parse_block);
-}
-
-// count: 0 none, 1 per-chunk counts, 2 counts + per-packet chunk ranks
-ParseKernel pick_parse(const yrss_ctx *c, int count, bool filter)
-{
-    return count == 2 ? pick_fn<2>(c, filter) : count == 1 ? pick_fn<1>(c, filter)
-                                                           : pick_fn<0>(c, filter);
+        return count == 2 ? yrss_parse_hash<2, true, kParseBlock>
+               : count    ? yrss_parse_hash<1, true, kParseBlock>
+                          : yrss_parse_hash<0, true, kParseBlock>;
+    return count == 2 ? yrss_parse_hash<2, false, kParseBlock>
+           : count    ? yrss_parse_hash<1, false, kParseBlock>
+                      : yrss_parse_hash<0, false, kParseBlock>;
 }
 
 hipEvent_t take_event(yrss_ctx *c)
@@ -2725,7 +2243,7 @@ hipEvent_t take_event(yrss_ctx *c)
         // this device, and the host synchronises on the stream anyway.  The
         // default system-scope fence writes back L2 at each timed kernel's end.
         hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, c->event_flags) != hipSuccess)
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess)
             return nullptr;
         return e;
     }
@@ -2920,20 +2438,41 @@ uint64_t mono_ns()
 yrss_ctx *g_dispatch_ctx = nullptr;
 std::mutex g_dispatch_mu;
 
-// A scan look-back that never resolved leaves that batch's lists invalid.
-bool take_scan_fault(yrss_ctx *c)
+const char *fault_name(uint32_t code)
 {
-    const uint32_t f = __atomic_exchange_n(c->d_scan_fault, 0u, __ATOMIC_ACQ_REL);
-    if (f)
-        fprintf(stderr, "yrss: scan look-back did not resolve; per-queue lists invalid\n");
-    return f != 0;
+    switch (code) {
+    case YRSS_FAULT_SCAN_TIMEOUT: return "scan look-back did not resolve";
+    case YRSS_FAULT_LIST_RANGE: return "list slot outside the batch";
+    case YRSS_FAULT_COUNT_MISMATCH: return "span histogram differs from the parse counts";
+    case YRSS_FAULT_COUNT_SLOT: return "parse count slot outside the wave's LDS";
+    case YRSS_FAULT_STAGE: return "stage slot outside the piece";
+    default: return "unknown";
+    }
+}
+
+// A device-side guard that fired (the fault record is set) leaves that
+// batch's per-queue lists invalid; q and hash are not affected.  Copies the
+// record to *out (if given) and clears it.  The caller has synchronised.
+bool take_fault(yrss_ctx *c, yrss_fault *out = nullptr)
+{
+    uint32_t *r = c->d_fault_rec;
+    const yrss_fault f{__atomic_load_n(r, __ATOMIC_ACQUIRE), r[1], r[2], r[3]};
+    if (out)
+        *out = f;
+    if (!f.code)
+        return false;
+    fprintf(stderr, "yrss: device fault %u (%s) in %s at %u (value %u); per-queue lists invalid\n",
+            f.code, fault_name(f.code), yrss_kernel_name((int)f.kernel), f.where, f.value);
+    r[1] = r[2] = r[3] = 0u;
+    __atomic_store_n(r, 0u, __ATOMIC_RELEASE);
+    return true;
 }
 
 int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream);
 
 bool small_ok(const yrss_ctx *c, uint32_t n)
 {
-    return !c->no_small && n >= 1 && n <= kSmallMaxPkts && c->nb <= kSmallMaxNb;
+    return c->tune.one_launch != 2 && n >= 1 && n <= kSmallMaxPkts && c->nb <= kSmallMaxNb;
 }
 
 // One launch of yrss_burst_small on the context stream.  S.P.win/len and the
@@ -2954,12 +2493,13 @@ int small_launch(yrss_ctx *c, SmallParams &S, bool filter, bool host_burst = tru
     P.mod_m = proto.mod_m;
     P.seg_cnt = nullptr;
     P.rank = nullptr;
+    P.fault = c->d_fault_rec;
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
     if (host_burst) {
-        S.done = c->spin_wait ? c->dh_done : nullptr;
+        S.done = c->dh_done;
         S.seq = ++c->done_seq;
-        c->pend.done_seq = c->spin_wait ? S.seq : 0u;   // the caller reset pend before
+        c->pend.done_seq = S.seq;   // the caller reset pend before
         stream = c->stream;
     } else {
         S.done = nullptr;
@@ -3002,7 +2542,7 @@ int finish_burst(yrss_ctx *c)
         YRSS_HIP(hipStreamSynchronize(c->stream));
     if (p.gather_fault && __atomic_load_n(c->h_fault, __ATOMIC_ACQUIRE))
         return -EFAULT;
-    if (p.scan_fault && take_scan_fault(c))
+    if (p.dev_fault && take_fault(c))
         return -EIO;
     for (int k = 0; k < 5; ++k)
         if (p.outs[k].user && !p.outs[k].direct)
@@ -3077,7 +2617,7 @@ int classify_staged(yrss_ctx *c, uint32_t n, uint32_t W, int16_t *out_q, uint32_
         YRSS_HIP(hipMemcpyAsync(c->h_qstart, c->d_qstart, (c->nb + 1) * 4,
                                 hipMemcpyDeviceToHost, s));
     }
-    p.scan_fault = compact;
+    p.dev_fault = compact;
     p.active = true;
     return 0;
 }
@@ -3148,6 +2688,8 @@ const char *yrss_kernel_name(int k)
     case YRSS_K_PARSE_HASH: return "yrss_parse_hash";
     case YRSS_K_SCAN: return "yrss_seg_scan";
     case YRSS_K_SCATTER: return "yrss_scatter";
+    case YRSS_K_BURST: return "yrss_burst_small";
+    case YRSS_K_WORKER: return "yrss_burst_worker";
     default: return "";
     }
 }
@@ -3216,80 +2758,8 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     c->cfg = *cfg;
     c->device = cfg->device;
     c->cus = prop.multiProcessorCount;
-    if (const char *e = getenv("YRSS_BLOCK")) {
-        const int v = atoi(e);
-        if (v == 256 || v == 512)
-            c->parse_block = (uint32_t)v;
-    }
-    if (const char *e = getenv("YRSS_NT"))
-        c->nt = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_CHUNK_TILES")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= 4096)
-            c->chunk_tiles = (uint32_t)v;
-    }
-    if (const char *e = getenv("YRSS_NO_RANK"))
-        c->no_rank = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_NO_IMG"))
-        c->no_img = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_NO_SINGLE"))
-        c->no_single = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_NO_COUNT"))
-        c->no_count = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_COUNT_MAXNB")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= YRSS_MAX_QUEUES + 1)
-            c->count_max_nb = (uint32_t)v;
-    }
-    if (const char *e = getenv("YRSS_RANK_IMG"))
-        c->rank_img = atoi(e) != 0 ? 1 : 0;
-    if (const char *e = getenv("YRSS_SCATTER_FULL"))
-        c->scatter_full = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_COUNT_KMIN")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= 256)
-            c->count_kmin = (uint32_t)v;
-    }
-    if (const char *e = getenv("YRSS_SCATTER_WPB")) {
-        const int v = atoi(e);
-        if (v == 1 || v == 2 || v == 4)
-            c->scatter_wpb = (uint32_t)v;
-    }
-    if (const char *e = getenv("YRSS_RANK_GSTAGE"))
-        c->rank_gstage = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_RANK_MINNB")) {
-        const int v = atoi(e);
-        if (v >= 2 && v <= YRSS_MAX_QUEUES + 1)
-            c->rank_min_nb = (uint32_t)v;
-    }
-    if (const char *e = getenv("YRSS_SCATTER_XCD"))
-        c->scatter_xcd = atoi(e) != 0 ? 1 : 0;
-    if (const char *e = getenv("YRSS_GROUP_TILES")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= 65536)
-            c->group_tiles = (uint32_t)v;
-    }
-    if (const char *e = getenv("YRSS_WAVES_PER_CU")) {
-        const int v = atoi(e);
-        if (v >= 4 && v <= kMaxWavesPerCU)
-            c->waves_per_cu = (uint32_t)v;
-    }
-    if (const char *e = getenv("YRSS_LDS_BLOCKS")) {
-        const int v = atoi(e);
-        if (v >= 1 && v <= 8)
-            c->lds_blocks = (uint32_t)v;
-    }
-    c->proto.out16 = 2;   // 16-byte sc1 bursts (profiles/r01_v13_ahead_out16_ab.log)
-    if (const char *e = getenv("YRSS_OUT16"))
-        c->proto.out16 = (uint32_t)std::min(2, std::max(0, atoi(e)));
-    if (const char *e = getenv("YRSS_NO_SMALL"))
-        c->no_small = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_SMALL_DEV"))
-        c->small_dev = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_SPIN_WAIT"))   // A/B: spin vs stream sync
-        c->spin_wait = atoi(e) != 0;
-    if (const char *e = getenv("YRSS_EVENT_FLAGS"))   // A/B of the timing-event fence
-        c->event_flags = (unsigned)strtoul(e, nullptr, 0);
+    c->tune.scatter_xcd = -1;
+    c->proto.out16 = 1;   // 16-byte write-through bursts (profiles/r01_v13_ahead_out16_ab.log)
     c->nb = (uint32_t)cfg->nb_queues + 1u;
     compute_key_schedule(cfg, c->proto.kwin);
     const bool only = cfg->soft_dispatch && cfg->dispatch_only_core;
@@ -3299,16 +2769,14 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     c->proto.nq = cfg->nb_queues;
     c->proto.nb = c->nb;
 
-    c->seg_cap = kMaxChunks;
-    const size_t ws = (size_t)c->seg_cap * c->nb * sizeof(uint32_t);
+    const size_t ws = (size_t)kMaxChunks * c->nb * sizeof(uint32_t);
     hipError_t e;
     if ((e = hipMalloc((void **)&c->d_seg_cnt, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_seg_off, ws)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_scan_status, (size_t)c->nb * (kMaxChunks / kScanTile) *
                                                        sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipHostMalloc((void **)&c->d_scan_fault, sizeof(uint32_t),
-                           hipHostMallocCoherent)) != hipSuccess ||
+        (e = hipHostMalloc((void **)&c->d_fault_rec, 64, hipHostMallocCoherent)) != hipSuccess ||
         (e = hipMemset(c->d_scan_status, 0, (size_t)c->nb * (kMaxChunks / kScanTile) *
                                                 sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_kni, sizeof(c->kni_bm))) != hipSuccess ||
@@ -3325,7 +2793,7 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         yrss_fini(c);
         return hip_fail("yrss_init allocation", e);
     }
-    *c->d_scan_fault = 0;
+    memset(c->d_fault_rec, 0, 64);
     *c->h_done = 0;
     // The memsets above run on the null stream, which does not order against
     // the context's non-blocking stream: without this wait a first dispatch
@@ -3372,7 +2840,7 @@ void yrss_fini(yrss_ctx *c)
     (void)hipFree(c->d_seg_off);
     (void)hipFree(c->d_scan_status);
     (void)hipFree(c->d_rank);
-    (void)hipHostFree(c->d_scan_fault);
+    (void)hipHostFree(c->d_fault_rec);
     (void)hipFree(c->d_totals);
     (void)hipFree(c->d_kni);
     (void)hipFree(c->d_fault);
@@ -3468,7 +2936,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     // lists in LDS) instead of parse + scan + scatter, ~10 us less per call
     // (profiles/r01_v26_small_kernel_stats.csv: three launches cost >= 15 us of
     // kernel time however small the batch).  Not timed by yrss_timing_*.
-    if (small_ok(c, n) && c->small_dev) {
+    if (small_ok(c, n) && c->tune.one_launch == 0) {
         SmallParams S;
         memset(&S, 0, sizeof(S));
         S.P.win = b->win;
@@ -3484,20 +2952,15 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     }
     const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
-    // Past 7 buckets (YRSS_RANK_MINNB), when count mode does not take the
-    // batch (8..256 buckets by default): the parse kernel also emits each
-    // packet's rank in its chunk and the scatter places it by that rank
-    // (group stage over the few-bucket path: +0.7-1 % at 8 buckets, +2-7 % at
-    // 9, -3 % at 6 and -5 % at 4: profiles/r02_v27_gstage3_ab.log,
-    // r02_v28_rankmin_ab.log).
-    // Measured against the ballot scatter: step -4 % at 33 buckets, -2 % at
-    // 17, +3 % at 65, +9 % at 129, even at 256; at 10 buckets (256-packet
-    // chunks) the ranks' cost in the parse kernel (+5-8 us) outweighed the
-    // gain, and chunks above kRankStage packets do not fit the stage.
-    const ScatterLds cl = compact ? count_lds(c, lay) : ScatterLds{};
-    const bool ranked =
-        compact && !c->no_rank && !cl.cnt_off && c->nb > c->rank_min_nb && lay.chunk <= kRankStage;
+    const uint64_t pwaves = (uint64_t)grid * (kParseBlock / kWave);
+    if (compact && ((uint64_t)lay.nchunk + pwaves - 1) / pwaves * c->nb > kCntWords)
+        return -EINVAL;   // layout_for sizes chunks so a wave's count slots fit
+    const ScatterLds sl = scatter_lds(c->nb, lay);
+    // the ranked scatter reads q as 16-byte vectors
+    const bool ranked = compact && sl.ranked && ((uintptr_t)b->q & 15u) == 0;
     if (ranked && c->rank_cap < n) {
+        // the ranks' workspace grows to the largest batch seen; the old one
+        // may still be read by a scatter queued on this stream
         if (c->d_rank) {
             YRSS_HIP(hipStreamSynchronize(s));
             (void)hipFree(c->d_rank);
@@ -3507,30 +2970,28 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         YRSS_HIP(hipMalloc((void **)&c->d_rank, (size_t)n * sizeof(uint16_t)));
         c->rank_cap = n;
     }
-
     ParseParams P = c->proto;
     P.win = b->win;
     P.len = b->len;
     P.q = b->q;
     P.hash = b->hash;
     P.seg_cnt = compact ? c->d_seg_cnt : nullptr;
+    P.rank = ranked ? c->d_rank : nullptr;
+    P.fault = c->d_fault_rec;
     P.n = n;
     P.stride = win_stride;
-    P.seg = lay.seg;
-    P.nseg = lay.nseg;
     P.chunk = lay.chunk;
     P.nchunk = lay.nchunk;
     P.ncol = lay.ncol;
     P.ct_shift = lay.ct_shift;
-    P.rank = ranked ? c->d_rank : nullptr;
     P.filter = b->filter;
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
     {
         Timed t(c, YRSS_K_PARSE_HASH);
-        hipExtLaunchKernelGGL(pick_parse(c, ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
-                              dim3(c->parse_block), (uint32_t)parse_lds(c, filter), s, t.a, t.b,
-                              0, P);
+        hipExtLaunchKernelGGL(pick_parse(ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
+                              dim3(kParseBlock),
+                              (uint32_t)parse_lds(filter), s, t.a, t.b, 0, P);
     }
     YRSS_HIP(hipGetLastError());
     if (!compact)
@@ -3542,7 +3003,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         SP.off = c->d_seg_off;
         SP.totals = c->d_totals;
         SP.status = c->d_scan_status;
-        SP.fault = c->d_scan_fault;
+        SP.fault = c->d_fault_rec;
         SP.nchunk = lay.nchunk;
         SP.ncol = lay.ncol;
         SP.tiles = lay.ncol / kScanTile;
@@ -3559,37 +3020,30 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.totals = c->d_totals;
     S.qidx = b->qidx;
     S.qstart = b->qstart;
+    S.fault = c->d_fault_rec;
     S.n = n;
     S.seg = lay.seg;
     S.nq = c->cfg.nb_queues;
     S.nb = c->nb;
-    S.nseg = lay.nseg;
     S.nchunk = lay.nchunk;
     S.ncol = lay.ncol;
     S.gshift = lay.shift;
-    S.chunk = lay.chunk;
-    S.rank = c->d_rank;
-    S.single = c->no_single ? 0u : 1u;
-    const ScatterLds sl = cl.cnt_off ? cl : scatter_lds(c, lay, ranked);
+    S.cshift = lay.ct_shift + 6u;
+    S.rank = ranked ? c->d_rank : nullptr;
     S.aux = sl.aux;
-    S.img = sl.img;
+    S.stg = sl.stg;
     S.wlds = sl.wlds;
-    S.cnt_off = sl.cnt_off;
-    S.kmin = c->count_kmin;
-    S.xcd = scatter_xcd_on(c) ? 1u : 0u;
-    S.gstage = ranked ? sl.gstage : 0u;
-    S.fault = c->d_scan_fault;
+    S.xcd = c->tune.scatter_xcd != 0 ? 1u : 0u;
     {
-        void (*fn)(ScatterParams) = ranked          ? yrss_scatter_ranked
-                                    : sl.m == 64u ? yrss_scatter<64>
-                                    : sl.m == 32u ? yrss_scatter<32>
-                                                  : yrss_scatter<0>;
+        // persistent: the resident workgroups only, never more than the spans
         const uint32_t lds = (uint32_t)(sl.wpb * sl.wlds * sizeof(uint32_t));
-        uint32_t grid = lay.nseg / sl.wpb;
-        if (!ranked && !c->scatter_full)   // persistent: the resident workgroups only
-            grid = std::min(grid, resident_blocks(c, (const void *)fn, sl.wpb * kWave, lds));
+        const uint32_t spans = (uint32_t)(((uint64_t)n + lay.seg - 1) / lay.seg);
+        uint32_t sgrid = (spans + sl.wpb - 1) / sl.wpb;
+        void (*fn)(ScatterParams) = ranked ? yrss_scatter<true> : yrss_scatter<false>;
+        sgrid = std::min(sgrid, resident_blocks(c, (const void *)fn, sl.wpb * kWave, lds));
         Timed t(c, YRSS_K_SCATTER);
-        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(sl.wpb * kWave), lds, s, t.a, t.b, 0, S);
+        hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(sl.wpb * kWave), lds, s, t.a,
+                              t.b, 0, S);
     }
     YRSS_HIP(hipGetLastError());
     return 0;
@@ -3942,7 +3396,7 @@ int zc_dispatch(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
         YRSS_HIP(hipMemcpyAsync(p.outs[k].direct ? p.outs[k].user : p.outs[k].stage, src[k],
                                 p.outs[k].bytes, hipMemcpyDeviceToHost, s));
     }
-    p.scan_fault = compact;
+    p.dev_fault = compact;
     p.active = true;
     return 0;
 }
@@ -4214,6 +3668,7 @@ int worker_launch(yrss_ctx *c)
     WorkerParams W;
     memset(&W, 0, sizeof(W));
     W.P = c->proto;
+    W.P.fault = c->d_fault_rec;
     W.P.kni_bm = c->d_kni;
     W.P.kni_enable = 0;
     const yrss_mbuf_layout &ml = c->cfg.mbuf;
@@ -4284,8 +3739,6 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
     const uint64_t life_ms = el ? strtoull(el, nullptr, 10) : 1000u;
     w.idle_ticks = std::min<uint64_t>(idle_ms, 10000u) * (uint64_t)khz;
     w.life_ticks = std::min<uint64_t>(std::max<uint64_t>(life_ms, 1u), 10000u) * (uint64_t)khz;
-    if (const char *e = getenv("YRSS_WORKER_POLL_SLEEP"))
-        w.poll_sleep = (uint32_t)std::min(std::max(atoi(e), 1), 256);
     const size_t S = nslots, M = kWorkerMaxBurst;
     hipError_t e;
     if ((e = hipStreamCreateWithFlags(&w.stream, hipStreamNonBlocking)) != hipSuccess ||
@@ -4459,6 +3912,8 @@ int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
     --w.pending;
     if (d & kWorkerFault)
         return -EFAULT;
+    if (__atomic_load_n(c->d_fault_rec, __ATOMIC_ACQUIRE) && take_fault(c))
+        return -EIO;   // a list guard fired in this (or an earlier) burst
     const size_t base = (size_t)si * kWorkerMaxBurst;
     if (o.copy & 1u)
         memcpy(o.q, w.q + base, (size_t)o.n * 2u);
@@ -4489,7 +3944,32 @@ int yrss_status(yrss_ctx *c)
         return -EINVAL;
     YRSS_HIP(hipSetDevice(c->device));
     YRSS_HIP(hipDeviceSynchronize());
-    return take_scan_fault(c) ? -EIO : 0;
+    return take_fault(c) ? -EIO : 0;
+}
+
+int yrss_fault_info(yrss_ctx *c, struct yrss_fault *out)
+{
+    if (!c || !out)
+        return -EINVAL;
+    YRSS_HIP(hipSetDevice(c->device));
+    YRSS_HIP(hipDeviceSynchronize());
+    (void)take_fault(c, out);
+    return 0;
+}
+
+int yrss_set_tuning(yrss_ctx *c, const struct yrss_tuning *t)
+{
+    if (!c || !t)
+        return -EINVAL;
+    const bool pow2 = (t->chunk_tiles & (t->chunk_tiles - 1u)) == 0 &&
+                      (t->span_tiles & (t->span_tiles - 1u)) == 0;
+    if (!pow2 || t->chunk_tiles > 4096u || t->span_tiles > 65536u || t->parse_blocks > 65536u ||
+        t->one_launch > 2u || t->scatter_xcd < -1 || t->scatter_xcd > 1)
+        return -EINVAL;
+    if (c->pend.active)
+        return -EBUSY;
+    c->tune = *t;
+    return 0;
 }
 
 int yrss_timing_enable(yrss_ctx *c, int enable)

@@ -124,6 +124,11 @@ class SoftRss:
     # -- lifetime ---------------------------------------------------------
     def close(self) -> None:
         if getattr(self, "_ctx", None) and self._ctx.value:
+            # a device guard that fired and was never read (yrss_status /
+            # fault_info) is logged before the context goes (abi.FAULT_LOG)
+            f = abi.Fault()
+            if self._lib.yrss_fault_info(self._ctx, ctypes.byref(f)) == 0 and f.code:
+                abi.FAULT_LOG.append((int(f.code), int(f.kernel), int(f.where), int(f.value)))
             self._lib.yrss_fini(self._ctx)
             self._ctx = ctypes.c_void_p()
 
@@ -411,9 +416,22 @@ class SoftRss:
 
     def status(self) -> int:
         """Synchronise and return (then clear) the device-side fault state:
-        0, or -EIO if the scan's look-back did not resolve or the ranked
-        scatter's index guard fired (yrss_status)."""
+        0, or -EIO if a list guard fired (yrss_status; details: fault_info)."""
         return int(self._lib.yrss_status(self._ctx))
+
+    def fault_info(self):
+        """Synchronise and return (then clear) the fault record as
+        (code, kernel, where, value); code 0 (abi.FAULT_NONE) = no guard fired."""
+        f = abi.Fault()
+        abi.check(self._lib.yrss_fault_info(self._ctx, ctypes.byref(f)), "yrss_fault_info")
+        return (int(f.code), int(f.kernel), int(f.where), int(f.value))
+
+    def set_tuning(self, chunk_tiles: int = 0, span_tiles: int = 0, parse_blocks: int = 0,
+                   one_launch: int = 0, scatter_xcd: int = -1) -> None:
+        """Layout overrides for tests and measurements (yrss_set_tuning); the
+        results never depend on them."""
+        t = abi.Tuning(chunk_tiles, span_tiles, parse_blocks, one_launch, scatter_xcd)
+        abi.check(self._lib.yrss_set_tuning(self._ctx, ctypes.byref(t)), "yrss_set_tuning")
 
     def grid_for(self, n: int) -> int:
         return int(self._lib.yrss_grid_for(self._ctx, n))
