@@ -29,6 +29,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PCIE_GEN5_X16_GBS = 64.0  # one direction of the host link, GB/s
 PROFILES = {"udp4_1flow": 0, "udp4": 1, "imix": 2, "vlan6_tcp": 3, "jumbo_tcp4": 4,
             "tcp4": 5, "fuzz": 6}
 WORKLOADS = {
@@ -353,11 +354,12 @@ def pcie_inclusive(profile: str):
                 continue
             out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
                         "mpps": d["mpps"], "note": d.get("note", "")})
-    # persistent worker, mbuf pointers and (data, data_len) pairs, one output set
-    # per ring slot: 32-packet bursts on 128 workgroups, 1024-packet bursts on 32
-    # (the best counts of the sweeps), ring depth 4 x workgroups
+    # persistent worker, mbuf pointers, (data, data_len) pairs and windows the
+    # dispatcher copies into a registered ring ("2"), one output set per ring
+    # slot: 32-packet bursts on 128 workgroups, 1024-packet bursts on 32 (the
+    # best counts of the sweeps), ring depth 4 x workgroups
     for frames, burst, blocks in (("0", 32, 128), ("0", 1024, 32), ("1", 32, 128),
-                                  ("1", 1024, 32)):
+                                  ("1", 1024, 32), ("2", 32, 128), ("2", 1024, 32)):
         try:
             r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
@@ -373,8 +375,15 @@ def pcie_inclusive(profile: str):
                 d = json.loads(line)
             except ValueError:
                 continue
+            # bytes crossing PCIe per packet, GPU reads: mbuf pointer 8 +
+            # header 64 + window 64 (64-byte packets), or pointer 8 + len 2 +
+            # window 64, or len 2 + window 64; writes q 2 + hash 4 + qidx 4
+            rd = {"0": 136, "1": 74, "2": 66}[frames]
+            gbs = d["mpps"] * 1e6 * (rd + 10) / 1e9
             out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
-                        "blocks": d.get("blocks"), "mpps": d["mpps"], "note": d.get("note", "")})
+                        "blocks": d.get("blocks"), "mpps": d["mpps"], "note": d.get("note", ""),
+                        "link_bytes_per_pkt": rd + 10, "link_GBps": round(gbs, 2),
+                        "link_frac": round(gbs / PCIE_GEN5_X16_GBS, 4)})
     return out or None
 
 

@@ -458,6 +458,18 @@ int yrss_worker_submit(yrss_ctx *ctx, void *const *mbufs, uint32_t n, int16_t *o
 int yrss_worker_submit_frames(yrss_ctx *ctx, const uint8_t *const *data, const uint16_t *len,
                               uint32_t n, int16_t *out_q, uint32_t *out_hash,
                               uint32_t *out_qidx, uint32_t *out_qstart, uint64_t *ticket);
+/* Same for windows the caller has copied, contiguously, into registered
+ * memory: window i at win + i * stride holds the first min(len[i], stride)
+ * bytes of packet i's first segment (stride >= 64, a multiple of 16; 80 never
+ * truncates).  The GPU reads the burst as one stretch of host memory, with no
+ * per-packet pointer reads: the dispatcher lcore's copy of each window (cache
+ * hot after rte_eth_rx_burst) replaces the GPU's dependent PCIe reads of the
+ * pointer array and then each scattered window.  -EFAULT if the windows are
+ * not in registered memory. */
+int yrss_worker_submit_windows(yrss_ctx *ctx, const uint8_t *win, uint32_t stride,
+                               const uint16_t *len, uint32_t n, int16_t *out_q,
+                               uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                               uint64_t *ticket);
 /* 0: the burst is done and its outputs in place; -EAGAIN: not yet (wait = 0);
  * -EFAULT: a mbuf or its data lies outside every registered range;
  * -ETIMEDOUT: waited 10 s (a burst takes microseconds: the GPU is hung). */

@@ -154,6 +154,41 @@ def test_worker_frames(dev, oracle_mod):
         eng.unregister_host_memory(pool.ctypes.data)
 
 
+@pytest.mark.parametrize("stride", [80, 96, 128])
+def test_worker_windows(dev, oracle_mod, stride):
+    """yrss_worker_submit_windows: the caller copied each packet's first
+    min(len, 80) bytes into registered staging (window i at i * stride); the
+    GPU reads only the staging, bit-identical to the frames form."""
+    cfg = (8, 8, 1, 0)
+    sizes = [32, 1, 1024, 500, 0, 77, 1000]
+    frames = _frames(oracle_mod, sum(sizes), 56 + stride)
+    q_all, h_all, _, _ = _expect(oracle_mod, frames, cfg)
+    lens = np.array([len(f) for f in frames], np.uint16)
+    raw = np.zeros(len(frames) * stride + 128, np.uint8)
+    win = raw[(-raw.ctypes.data) % 64:]                      # 64-byte aligned staging
+    for i, f in enumerate(frames):
+        w = bytes(f[:80])
+        win[i * stride:i * stride + len(w)] = np.frombuffer(w, np.uint8)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(raw.ctypes.data, raw.nbytes)
+        eng.worker_start(8, 2)
+        off = 0
+        for n in sizes:
+            view = win[off * stride:]
+            t = eng.worker_submit_windows(view, stride, lens[off:off + n])
+            r = eng.worker_poll(t)
+            qr = q_all[off:off + n]
+            qi_ref, qs_ref = oracle_mod.process_burst(qr, cfg[1])
+            assert np.array_equal(r.queue, qr) and np.array_equal(r.hash, h_all[off:off + n])
+            assert np.array_equal(r.qidx, qi_ref)
+            assert np.array_equal(r.qstart[: qs_ref.size], qs_ref)
+            off += n
+        with pytest.raises(abi.YrssError):
+            eng.worker_submit_windows(win, 0, lens[:4])       # stride below a window
+        eng.worker_stop()
+        eng.unregister_host_memory(raw.ctypes.data)
+
+
 def test_worker_low_rate_no_stall(dev, oracle_mod, monkeypatch):
     """Fewer than B bursts per idle period: idle is judged over the whole
     ring, so no workgroup leaves while the others keep serving (its tickets

@@ -59,8 +59,11 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
                       double secs, int16_t *q_all, uint32_t *h_all, uint32_t *qi_all,
                       uint32_t profile, int thp, const uint8_t **fdata, uint16_t *flen)
 {
+    /* YRSS_CBENCH_WORKER_FRAMES: 0 mbuf pointers, 1 (data, data_len) pairs,
+     * 2 windows the dispatcher copies into a registered staging ring
+     * (yrss_worker_submit_windows) */
     const char *fe = getenv("YRSS_CBENCH_WORKER_FRAMES");
-    const int frames = fe && atoi(fe) != 0;
+    const int frames = fe ? atoi(fe) : 0;
     if (frames)
         fill_frames(mbufs, pool, fdata, flen);   /* outside the timed region */
     const char *so = getenv("YRSS_CBENCH_WORKER_SLOTOUT");
@@ -80,8 +83,12 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
     cfg.max_burst = 0;
     yrss_ctx *ctx = NULL;
     int rc;
+    /* windows form: one staging stretch of B windows per ring slot */
+    const size_t wst_sz = frames == 2 ? ((size_t)depth * B * YRSS_WIN_FULL + 4095) & ~(size_t)4095 : 0;
+    uint8_t *wst = wst_sz ? aligned_alloc(4096, wst_sz) : NULL;
     if ((rc = yrss_init(&cfg, &ctx)) || (rc = yrss_register_host_memory(ctx, mem, mem_sz)) ||
         (rc = yrss_register_host_memory(ctx, arena, arena_sz)) ||
+        (wst && (rc = yrss_register_host_memory(ctx, wst, wst_sz))) ||
         (rc = yrss_worker_start(ctx, depth, blocks))) {
         fprintf(stderr, "worker setup: %d\n", rc);
         return 2;
@@ -110,10 +117,23 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
             /* YRSS_CBENCH_WORKER_SLOTOUT=1: one fixed output set per ring slot (the
              * F-Stack pattern), else outputs follow the packets through the arena */
             const size_t oo = slotout ? (size_t)k * B : off;
-            rc = frames ? yrss_worker_submit_frames(ctx, fdata + off, flen + off, B, q_all + oo,
-                                                    h_all + oo, qi_all + oo, qs[k], &tk[k])
-                        : yrss_worker_submit(ctx, mbufs + off, B, q_all + oo, h_all + oo,
-                                             qi_all + oo, qs[k], 0, &tk[k]);
+            if (frames == 2) {
+                /* the dispatcher's copy of the burst's windows (cache hot after
+                 * rte_eth_rx_burst in F-Stack) is part of the timed work */
+                uint8_t *w = wst + (size_t)k * B * YRSS_WIN_FULL;
+                for (uint32_t j = 0; j < B; ++j) {
+                    const uint32_t L = flen[off + j] < YRSS_WIN_FULL ? flen[off + j] : YRSS_WIN_FULL;
+                    memcpy(w + (size_t)j * YRSS_WIN_FULL, fdata[off + j], L);
+                }
+                rc = yrss_worker_submit_windows(ctx, w, YRSS_WIN_FULL, flen + off, B, q_all + oo,
+                                                h_all + oo, qi_all + oo, qs[k], &tk[k]);
+            } else {
+                rc = frames ? yrss_worker_submit_frames(ctx, fdata + off, flen + off, B,
+                                                        q_all + oo, h_all + oo, qi_all + oo,
+                                                        qs[k], &tk[k])
+                            : yrss_worker_submit(ctx, mbufs + off, B, q_all + oo, h_all + oo,
+                                                 qi_all + oo, qs[k], 0, &tk[k]);
+            }
             cyc_poll += c1 - c0;
             cyc_sub += __rdtsc() - c1;
             ++nb;
@@ -140,14 +160,17 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
            "\"poll_cycles\": %.0f, \"submit_cycles\": %.0f, "
            "\"mode\": 4, \"note\": \"persistent kernel polls a ring of bursts in pinned "
            "memory; %s read over PCIe\"}\n",
-           frames ? "yrss_worker_submit_frames" : "yrss_worker_submit", profile, B, depth,
+           frames == 2 ? "yrss_worker_submit_windows"
+           : frames    ? "yrss_worker_submit_frames" : "yrss_worker_submit", profile, B, depth,
            blocks, (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
            (t1 - t0) / (pkts / (double)B) * 1e6, thp, nb ? (double)cyc_poll / nb : 0.0,
            nb ? (double)cyc_sub / nb : 0.0,
-           frames ? "windows of (data, data_len) pairs" : "mbuf headers + windows");
+           frames == 2 ? "contiguous windows the dispatcher copied (one stretch per burst)"
+           : frames    ? "windows of (data, data_len) pairs" : "mbuf headers + windows");
     fflush(stdout);
     free(tk);
     yrss_fini(ctx);
+    free(wst);
     return 0;
 }
 

@@ -188,6 +188,8 @@ _PROTOS = {
                                           ctypes.POINTER(ctypes.c_uint64)]),
     "yrss_worker_submit_frames": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp,
                                                  ctypes.POINTER(ctypes.c_uint64)]),
+    "yrss_worker_submit_windows": (ctypes.c_int, [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp,
+                                                  ctypes.POINTER(ctypes.c_uint64)]),
     "yrss_worker_poll": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_int]),
     "yrss_worker_stop": (ctypes.c_int, [_vp]),
     "yrss_dispatch_frames_zc_ex": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp,

@@ -51,12 +51,11 @@ constexpr int kTile = 64;              // packets per wave-tile (one per lane)
 constexpr int kScatterBlock = 256;     // 4 waves per scatter workgroup (halved for large nb)
 constexpr int kScatterWaves = kScatterBlock / kWave;
 constexpr uint32_t kMaxChunks = 65536;  // per launch; bounds the count matrix [nb][ncol]
-constexpr uint32_t kCntWords = 2048;    // parse: per-wave LDS count slots (chunks x nb)
+constexpr uint32_t kCntWords = 2176;    // parse: per-wave LDS count slots (chunks x nb): 32 x 68
 constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
 constexpr uint32_t kPiece = 2048;       // scatter: packets ranked and staged at once per wave
 constexpr uint32_t kPieceSlots = kPiece / 64;   // 64-packet slots of a piece
-constexpr uint32_t kImgLine = 32;       // list entries per 128-byte line
-constexpr uint32_t kTab = 16;           // ranked scatter: prefix-table words per lane (nb x 2nc <= 1024)
+constexpr uint32_t kTab = 17;           // ranked scatter: prefix-table words per lane (nb x 2nc <= 1088)
 // Toeplitz key tables: the 96 tuple bits are cut into 12 bytes (MSB first);
 // table t maps a byte value to the XOR of the key windows its set bits select
 // (12 lookups per hash).  Nibble tables (24 conflict-free lookups) and
@@ -680,12 +679,17 @@ constexpr uint64_t kStFlagP = 1ull << 63;   // status holds the inclusive prefix
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
 {
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, kWave);
-        if (lane >= (uint32_t)d)
-            x += y;
-    }
+    // DPP: Hillis-Steele inside each 16-lane row (row_shr 1, 2, 4, 8), then
+    // row 0's last lane into row 1, rows 0-1's into rows 2-3 (row_bcast 15,
+    // 31 of the gfx9 DPP set): six VALU ops and no LDS round trip, where
+    // shuffles cost a ds_bpermute and its wait per step
+    (void)lane;
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);   // row_bcast:31
     return x;
 }
 
@@ -879,12 +883,35 @@ __device__ __forceinline__ void rank_piece(const ScatterParams &P,
 // Writes a piece's stage out, quad by quad: four words of one bucket are one
 // aligned 16-byte store (non-temporal when the piece writes the whole line),
 // others word by word.  Returns how many entries this lane wrote.
+#ifndef YRSS_AB_STORE
+#define YRSS_AB_STORE 0
+#endif
 __device__ __forceinline__ uint32_t copy_out(const ScatterParams &P, const uint32_t *stg,
                                              const uint32_t *base, const uint32_t *ls,
                                              const uint32_t *cnt, uint32_t p0, uint32_t ph,
                                              uint32_t lane)
 {
     uint32_t wrote = 0;
+#if YRSS_AB_STORE == 5 || YRSS_AB_STORE == 6
+    for (uint32_t k = lane; k < P.stg; k += kWave) {
+        const uint32_t w = stg[k], bk = w & 511u;
+        if (bk >= P.nb)
+            continue;
+        const uint32_t kk = k - ls[bk], d = base[bk] + kk;
+        if (kk < cnt[bk] && d < P.n) {
+#if YRSS_AB_STORE == 5
+            __builtin_nontemporal_store(p0 + (w >> 9), P.qidx + d);
+#else
+            P.qidx[d] = p0 + (w >> 9);
+#endif
+            ++wrote;
+        } else {
+            report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, p0 + (w >> 9), d);
+        }
+    }
+    (void)ph;
+    return wrote;
+#endif
     for (uint32_t v = lane; v < P.stg / 4u; v += kWave) {
         const u32x4 e = reinterpret_cast<const u32x4 *>(stg)[v];
         const uint32_t b = e.x & 511u;
@@ -895,21 +922,13 @@ __device__ __forceinline__ uint32_t copy_out(const ScatterParams &P, const uint3
             if (k0 + 3u < cnt[b] && d + 4u <= P.n && d + 4u > d) {
                 const u32x4 x = {p0 + (e.x >> 9), p0 + (e.y >> 9), p0 + (e.z >> 9),
                                  p0 + (e.w >> 9)};
-                const uint32_t la = (d + ph) & ~(kImgLine - 1u);   // line, in address units
-                u32x4 *dst = reinterpret_cast<u32x4 *>(P.qidx + d);
-#ifndef YRSS_AB_STORE
-#define YRSS_AB_STORE 0
-#endif
-                if (YRSS_AB_STORE == 1)
-                    *dst = x;
-                else if (YRSS_AB_STORE == 2)
-                    __builtin_nontemporal_store(x, dst);
-                else if (YRSS_AB_STORE == 3)
-                    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(x) : "memory");
-                else if (la >= bs + ph && la + kImgLine <= bs + cnt[b] + ph)
-                    __builtin_nontemporal_store(x, dst);
-                else
-                    *dst = x;
+                // non-temporal, whole lines and the partial lines at a run's
+                // ends alike: plain stores for the partial lines left them
+                // dirty in L2, written back inside the next batch's parse
+                // kernel (+14 us there at 9 buckets, same box,
+                // profiles/r03_ab_store.log); write-through (sc1) stores cost
+                // the scatter 1.7-3.8x
+                __builtin_nontemporal_store(x, reinterpret_cast<u32x4 *>(P.qidx + d));
                 wrote += 4u;
             } else {
                 report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, p0 + (e.x >> 9), d);
@@ -923,7 +942,11 @@ __device__ __forceinline__ uint32_t copy_out(const ScatterParams &P, const uint3
                 const uint32_t kk = 4u * v + k - ls[bk];
                 const uint32_t d = base[bk] + kk;
                 if (kk < cnt[bk] && d < P.n) {
+#if YRSS_AB_STORE == 4
+                    __builtin_nontemporal_store(p0 + (w >> 9), P.qidx + d);
+#else
                     P.qidx[d] = p0 + (w >> 9);
+#endif
                     ++wrote;
                 } else {
                     report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, p0 + (w >> 9),
@@ -1105,11 +1128,11 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
             wave_lds_sync();
             layout();
             wave_lds_sync();
-            for (uint32_t b = lane; b < P.nb; b += kWave) {
-                uint32_t *t = tab + (b << lcp);
-                const uint32_t l = ls[b], o0 = t[0];
-                for (uint32_t c = 0; c < nc; ++c)
-                    t[c] = l + t[c] - o0;
+            // off = ls[b] + prefix - prefix at the span's first chunk (=
+            // base[b] - start[b]), every entry in parallel
+            for (uint32_t e = lane; e < ntab; e += kWave) {
+                const uint32_t b = e >> lcp;
+                tab[e] = ls[b] + tab[e] - (base[b] - start[b]);
             }
             wave_lds_sync();
             // place: stage slot = off[bucket][chunk] + rank, entry (packet -
@@ -1717,7 +1740,9 @@ struct alignas(64) WorkerSlot {
     // caller's own arrays when they lie in registered memory (no copy at
     // poll), else the slot's staging; 0 = not wanted
     uint64_t out[4];
-    uint64_t pad_[2];
+    uint64_t win;        // windows form: device address of window 0 (stride below)
+    uint32_t stride;
+    uint32_t pad_;
 };
 // done[slot] = ticket | kWorkerFault when a pointer was outside every range.
 // Consecutive slots share a line, so a host polling in ticket order misses
@@ -1728,6 +1753,7 @@ constexpr uint64_t kWorkerFault = 1ull << 63;
 constexpr uint32_t kWorkerSameOut = 1u << 17;
 constexpr uint32_t kWorkerOutCache = 32;   // cached slots per workgroup (LDS)
 constexpr uint32_t kWorkerFrames = 1u << 16;   // slot holds (data, data_len) pairs
+constexpr uint32_t kWorkerWindows = 1u << 18;  // slot names contiguous windows (win, stride)
 static_assert(sizeof(WorkerSlot) == 64, "one line per slot header");
 
 // Launch control, host-coherent.  Line 0 is written by the host only (so
@@ -1860,6 +1886,14 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
                     ctl[4 + 2 * k] = (uint32_t)o[k];
                     ctl[5 + 2 * k] = (uint32_t)(o[k] >> 32);
                 }
+                if (ctl[2] & kWorkerWindows) {
+                    const uint64_t wb = __hip_atomic_load(&sl->win, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_SYSTEM);
+                    ctl[12] = (uint32_t)wb;
+                    ctl[13] = (uint32_t)(wb >> 32);
+                    ctl[14] = __hip_atomic_load(&sl->stride, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
             ctl[0] = go;
         }
@@ -1882,14 +1916,25 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         P.rank = nullptr;
         P.out16 = 0;
         const uint32_t frames = (ctl[2] & kWorkerFrames) ? 1u : 0u;
+        const bool windows = (ctl[2] & kWorkerWindows) != 0;
+        if (windows) {
+            // the caller copied the burst's windows contiguously into
+            // registered memory: the parse reads them in place, one stretch
+            // of host memory, with no pointer reads and no gather
+            P.win = reinterpret_cast<const uint8_t *>(((uint64_t)ctl[13] << 32) | ctl[12]);
+            P.stride = ctl[14];
+            P.len = W.lens + (size_t)si * kWorkerMaxBurst;
+        }
         const GatherIO gio{W.ptrs + (size_t)si * kWorkerMaxBurst,
                            W.lens + (size_t)si * kWorkerMaxBurst, const_cast<uint8_t *>(P.win),
                            const_cast<uint16_t *>(P.len), W.fault + blockIdx.x, n, frames};
         if (n) {
             small_burst_body<false, 1>(P, W.G, gio,
                                     BurstIO{static_cast<uint32_t *>(out_ptr(2)),
-                                            static_cast<uint32_t *>(out_ptr(3)), 1u,
-                                            (!frames && (ctl[2] & YRSS_F_WRITE_RSS)) ? 1u : 0u},
+                                            static_cast<uint32_t *>(out_ptr(3)),
+                                            windows ? 0u : 1u,
+                                            (!frames && !windows && (ctl[2] & YRSS_F_WRITE_RSS))
+                                                ? 1u : 0u},
                                     L, wave, lane);
         } else if (threadIdx.x <= W.P.nb && out_ptr(3)) {
             static_cast<uint32_t *>(out_ptr(3))[threadIdx.x] = 0u;
@@ -2157,9 +2202,9 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     const uint64_t max_chunks = std::min<uint64_t>(kMaxChunks, waves * slots);
     const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
     // the ranked scatter keeps 2 x (span chunks) prefixes per bucket (at most
-    // 64 kTab words a wave): 4-tile chunks up to 64 buckets, 8 to 128, 16 to
-    // 256, 32 (one chunk a span) past that
-    const uint64_t ct_nb = c->nb <= 64u ? 4u : c->nb <= 128u ? 8u : c->nb <= 256u ? 16u : 32u;
+    // 64 kTab words a wave): 4-tile chunks up to 68 buckets (64 lcores and
+    // the drop bucket), 8 to 136, 16 to 272 (every bucket count)
+    const uint64_t ct_nb = c->nb <= 68u ? 4u : c->nb <= 136u ? 8u : 16u;
     uint64_t ct = std::max<uint64_t>(c->tune.chunk_tiles ? c->tune.chunk_tiles : ct_nb,
                                      (tiles + max_chunks - 1) / max_chunks);
     uint32_t ct_shift = 0;
@@ -3116,7 +3161,7 @@ int yrss_set_dispatch_ctx(yrss_ctx *c)
 namespace {
 int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
                   int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
-                  uint32_t flags, uint64_t *ticket);
+                  uint32_t flags, uint64_t *ticket, uint64_t win = 0, uint32_t stride = 0);
 
 // The shim's packet as a one-packet burst of the context's resident worker:
 // its window (the at most YRSS_WIN_FULL bytes the GPU reads) is copied into a
@@ -3796,7 +3841,7 @@ namespace {
 
 int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t n,
                   int16_t *out_q, uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
-                  uint32_t flags, uint64_t *ticket)
+                  uint32_t flags, uint64_t *ticket, uint64_t win, uint32_t stride)
 {
     auto &w = c->w;
     if (!w.on)
@@ -3808,7 +3853,10 @@ int worker_submit(yrss_ctx *c, const void *ptrs, const uint16_t *lens, uint32_t 
     if (!w.out[si].collected)
         return -EBUSY;   // the slot's previous ticket was not polled yet
     WorkerSlot *sl = w.slots + si;
-    memcpy(w.ptrs + (size_t)si * kWorkerMaxBurst, ptrs, (size_t)n * 8u);
+    if (ptrs)
+        memcpy(w.ptrs + (size_t)si * kWorkerMaxBurst, ptrs, (size_t)n * 8u);
+    sl->win = win;
+    sl->stride = stride;
     if (lens)
         memcpy(w.lens + (size_t)si * kWorkerMaxBurst, lens, (size_t)n * 2u);
     // Outputs the caller keeps in registered memory are written there by the
@@ -3879,6 +3927,21 @@ int yrss_worker_submit_frames(yrss_ctx *c, const uint8_t *const *data, const uin
         return -EINVAL;
     return worker_submit(c, data, len, n, out_q, out_hash, out_qidx, out_qstart, kWorkerFrames,
                          ticket);
+}
+
+int yrss_worker_submit_windows(yrss_ctx *c, const uint8_t *win, uint32_t stride,
+                               const uint16_t *len, uint32_t n, int16_t *out_q,
+                               uint32_t *out_hash, uint32_t *out_qidx, uint32_t *out_qstart,
+                               uint64_t *ticket)
+{
+    if (!c || !ticket || (n && (!win || !len || !out_q)) || stride < YRSS_WIN_MIN ||
+        (stride & 15u) || ((uintptr_t)win & 15u))
+        return -EINVAL;
+    const void *dw = n ? dev_alias(c, win, (size_t)n * stride) : win;
+    if (!dw)
+        return -EFAULT;   // the windows must lie in registered memory
+    return worker_submit(c, nullptr, len, n, out_q, out_hash, out_qidx, out_qstart,
+                         kWorkerWindows, ticket, (uint64_t)(uintptr_t)dw, stride);
 }
 
 int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)

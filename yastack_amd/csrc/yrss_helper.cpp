@@ -99,7 +99,6 @@ int main(int argc, char **argv)
     }
     __atomic_store_n(&h->ready, 1, __ATOMIC_RELEASE);
 
-    std::vector<const uint8_t *> ptrs(h->max_burst);
     std::deque<Pending> inflight;
     uint64_t next = __atomic_load_n(&h->first, __ATOMIC_ACQUIRE);
     uint32_t idle = 0;
@@ -115,11 +114,11 @@ int main(int argc, char **argv)
                 break;
             const uint32_t n = slots[si].n;
             uint8_t *d = data(si);
-            for (uint32_t i = 0; i < n; ++i)
-                ptrs[i] = d + a.win + (size_t)i * kWin;
             uint64_t wt = 0;
-            rc = yrss_worker_submit_frames(
-                ctx, ptrs.data(), reinterpret_cast<const uint16_t *>(d + a.len), n,
+            // the slot's windows are contiguous (stride 80) in registered
+            // memory: the GPU reads them as one stretch
+            rc = yrss_worker_submit_windows(
+                ctx, d + a.win, kWin, reinterpret_cast<const uint16_t *>(d + a.len), n,
                 reinterpret_cast<int16_t *>(d + a.q), reinterpret_cast<uint32_t *>(d + a.hash),
                 reinterpret_cast<uint32_t *>(d + a.qidx),
                 reinterpret_cast<uint32_t *>(d + a.qstart), &wt);

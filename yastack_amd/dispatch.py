@@ -295,6 +295,25 @@ class SoftRss:
                                            None if qi is None else qi[:n], qs)
         return t.value
 
+    def worker_submit_windows(self, win: np.ndarray, stride: int, lens: np.ndarray,
+                              want_hash=True, compact=True) -> int:
+        """Queue one burst of contiguous windows (window i at win[i * stride:])
+        that lie in registered memory (``yrss_worker_submit_windows``)."""
+        ln = np.ascontiguousarray(lens, dtype=np.uint16)
+        n = int(ln.size)
+        q = np.empty(max(n, 1), np.int16)
+        h = np.empty(max(n, 1), np.uint32) if want_hash else None
+        qi = np.empty(max(n, 1), np.uint32) if compact else None
+        qs = np.empty(self.nb_queues + 2, np.uint32) if compact else None
+        t = ctypes.c_uint64()
+        rc = self._lib.yrss_worker_submit_windows(self._ctx, _ptr(win), stride, _ptr(ln), n,
+                                                  _ptr(q), _ptr(h), _ptr(qi), _ptr(qs),
+                                                  ctypes.byref(t))
+        abi.check(rc, "yrss_worker_submit_windows")
+        self._wk[t.value] = DispatchResult(q[:n], None if h is None else h[:n],
+                                           None if qi is None else qi[:n], qs)
+        return t.value
+
     def toeplitz_dispatch(self, frame: bytes, queue_id: int = 0) -> int:
         """The per-packet registration shim (``yrss_toeplitz_dispatch``) on this
         context: ``toeplitz_dispatch``'s return value for one frame, computed on
