@@ -77,6 +77,9 @@ def parse_args(argv=None):
                          "(0: diagnosis only, roofline.achieved is then null)")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_parse_hash.json"),
                     help="rocprofv3 PMC summary used for roofline.traffic")
+    ap.add_argument("--tune", default="",
+                    help="layout overrides for measurements, k=v[,k=v] (yrss_set_tuning "
+                         "fields: chunk_tiles, span_tiles, parse_blocks, scatter_xcd)")
     ap.add_argument("--dry", action="store_true",
                     help="plumbing check without a GPU (rank spawn, barrier, reductions); "
                          "prints a line marked dry, never a measurement")
@@ -530,6 +533,8 @@ def main(argv=None):
     nbq = args.nb_queues or args.nb_procs
     eng = SoftRss(nb_procs=args.nb_procs, nb_queues=nbq, soft_dispatch=1,
                   dispatch_only_core=args.dispatch_only_core, device=local, max_burst=0)
+    if args.tune:
+        eng.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
     n = args.pkts
     nbat = max(1, args.batches)
     prof = PROFILES[args.profile]

@@ -179,9 +179,7 @@ def test_worker_windows(dev, oracle_mod, stride):
             r = eng.worker_poll(t)
             qr = q_all[off:off + n]
             qi_ref, qs_ref = oracle_mod.process_burst(qr, cfg[1])
-            assert np.array_equal(r.queue, qr) and np.array_equal(r.hash, h_all[off:off + n])
-            assert np.array_equal(r.qidx, qi_ref)
-            assert np.array_equal(r.qstart[: qs_ref.size], qs_ref)
+            _check(r, qr, h_all[off:off + n], qi_ref, qs_ref)
             off += n
         with pytest.raises(abi.YrssError):
             eng.worker_submit_windows(win, 0, lens[:4])       # stride below a window

@@ -39,6 +39,7 @@
 
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "yrss.h"
@@ -94,6 +95,7 @@ struct ParseParams {
     const uint32_t *kni_bm;   // tcp bitmap (2048 words) then udp bitmap (2048 words)
     uint32_t kni_enable;
     uint32_t out16;       // full output bursts as 16-byte write-through stores (0: lane-granular)
+    uint32_t rank_pack;   // kCount == 2: the rank word is bucket << (ct_shift + 6) | rank
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
@@ -515,7 +517,8 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
             if (leader)
                 before = atomicAdd(&cnt[bkt], (uint32_t)__popcll(peers));
             const int ll = peers ? __builtin_ctzll(peers) : (int)lane;
-            ob.r[lane] = (uint16_t)(__shfl(before, ll, kWave) + (uint32_t)__popcll(peers & lt));
+            const uint32_t tag = P.rank_pack ? bkt << (P.ct_shift + 6u) : 0u;
+            ob.r[lane] = (uint16_t)(tag | (__shfl(before, ll, kWave) + (uint32_t)__popcll(peers & lt)));
         } else if (leader) {
             atomicAdd(&cnt[bkt], (uint32_t)__popcll(peers));
         }
@@ -1235,6 +1238,407 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
             for (uint32_t k = 0; k < kPieceSlots; ++k)
                 qv[k] = qn[k];
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel 3 (ranked): the lists written in whole 64-byte lines.
+//
+// A workgroup takes one contiguous range of spans (a span: 2^gshift parse
+// chunks, up to kLineSpanMax packets) and works them in order.  Per span it
+// places every packet in an LDS stage by the parse kernel's rank (stage slot =
+// the bucket's position for its chunk + rank, the positions from the scan's
+// prefixes), the stage laid out line for line like the lists: bucket b's
+// words sit in stage lines of their own at their list address's phase inside
+// a 64-byte line.  Whole lines go out as 16-byte non-temporal stores, four
+// lanes to a line; the bucket's last line, when the span ends inside it, is
+// carried in LDS into the next span's stage and completed there, so inside a
+// workgroup's range every line leaves complete, once.  Only the first and last
+// line of each bucket in a range can be partial (word stores).  A list line
+// written in pieces costs a read-modify-write or a second partial write-back;
+// the per-wave scatter this replaces wrote ~30-word runs per span at 64
+// buckets and most of its lines in two pieces (r03 q-rows: 63 us scatter and
+// +14 us in the next parse kernel, against the list-write floor of ~15 us).
+//
+// The packets' (bucket, rank) come from the parse kernel's rank stream: packed
+// as bucket << cshift | rank when the bucket fits beside the rank (kPacked;
+// the scatter then reads 2 bytes a packet), else the rank beside q.  Checks: a
+// slot outside the stage lands in a spare word, every stage word is
+// pre-filled with 0xFFFFFFFF and a list word still holding it is a hole
+// (two packets on one slot), and the words a workgroup writes must add up to
+// its range's packets; each reports through the fault record instead of
+// storing (YRSS_FAULT_STAGE / _LIST_RANGE / _COUNT_MISMATCH).
+// ---------------------------------------------------------------------------
+constexpr int kLineBlock = 512;
+constexpr uint32_t kLineGroups = 2;                                 // 8-packet groups a thread
+constexpr uint32_t kLineSpanMax = kLineBlock * 8u * kLineGroups;   // 8192 packets
+constexpr uint32_t kLineTabRegs = 8;                                // prefix words a thread
+constexpr uint32_t kLineTabMax = kLineBlock * kLineTabRegs;        // nb x span chunks <= 4096
+constexpr uint32_t kHole = 0xFFFFFFFFu;
+
+struct LineParams {
+    const int16_t *q;          // !kPacked: the bucket of each packet
+    const uint16_t *rank;      // rank in chunk (kPacked: bucket << cshift | rank)
+    const uint32_t *seg_off;   // [nb][ncol] exclusive per-bucket prefix per chunk
+    const uint32_t *totals;    // [nb]
+    uint32_t *qidx;
+    uint32_t *qstart;          // [nb + 1]
+    uint32_t *fault;
+    uint32_t n, nq, nb, nchunk, ncol;
+    uint32_t seg;              // packets per span: 2^gshift chunks, <= kLineSpanMax
+    uint32_t gshift, cshift;   // span = 2^gshift chunks, chunk = 2^cshift packets
+    uint32_t lmax;             // stage lines: seg / 16 + 2 nb + 1
+    uint32_t xcd;              // workgroups of one XCD take consecutive ranges
+};
+
+// LDS of a workgroup, in words: per-bucket arrays, the prefix table, the
+// carried lines, the stage's line tags, the stage (+ a spare word).
+struct LineLds {
+    uint32_t start, cs, ve, ce, so, rb, tend, lsl, misc, tab, cb, ltag, lgl, stg, words;
+};
+__host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32_t lmax)
+{
+    LineLds L;
+    uint32_t o = 0;
+    auto take = [&](uint32_t w) {
+        const uint32_t at = o;
+        o = (o + w + 3u) & ~3u;
+        return at;
+    };
+    L.start = take(nb);
+    L.cs = take(nb);      // this span's first valid list position (adjusted), carry start
+    L.ve = take(nb);      // this span's end position (adjusted)
+    L.ce = take(nb);      // carry end = the span's first packet position (adjusted)
+    L.so = take(nb);      // stage index = so[b] + adjusted position
+    L.rb = take(nb);      // prefix table row bias (to stage slots)
+    L.tend = take(nb);    // prefix at the span's end
+    L.lsl = take(nb + 1u);   // first stage line of each bucket
+    L.misc = take(4);
+    L.tab = take(nb * ((1u << gshift) + 1u));   // rows of 2^gshift + 1 words (odd: banks)
+    L.cb = take(16u * nb);
+    L.ltag = take(lmax);  // bucket | copy mode << 30 per stage line
+    L.lgl = take(lmax);   // the line's list line (adjusted position / 16)
+    L.stg = take(16u * lmax + 4u);
+    L.words = o;
+    return L;
+}
+
+// 8 x 16-bit words per 16-byte load, groups k = 0, 1 of this thread: packets
+// p0 + 8 (512 k + t) ..+7; past pe read 0 (range check; a batch's last span
+// that ends inside a vector is read word by word, as the check drops a
+// partial vector whole).
+__device__ __forceinline__ void load_groups(const uint16_t *a, uint32_t p0, uint32_t pe,
+                                            uint32_t t, u32x4 (&v)[kLineGroups])
+{
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(a + p0), 0, (int)((pe - p0) * 2u), kRsrcWord3);
+    if (((pe - p0) & 7u) == 0) {
+#pragma unroll
+        for (uint32_t k = 0; k < kLineGroups; ++k)
+            v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 r, (int)((k * kLineBlock + t) * 16u), 0, 2));
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < kLineGroups; ++k) {
+            uint32_t w[4];
+#pragma unroll
+            for (uint32_t i = 0; i < 4u; ++i) {
+                const int o = (int)((k * kLineBlock + t) * 16u + 4u * i);
+                w[i] = __builtin_amdgcn_raw_buffer_load_b16(r, o, 0, 0) |
+                       ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 2, 0, 0) << 16);
+            }
+            v[k] = u32x4{w[0], w[1], w[2], w[3]};
+        }
+    }
+}
+
+template <bool kPacked>
+__global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
+    const uint32_t nb = P.nb, t = threadIdx.x, lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const LineLds o = line_lds(nb, P.gshift, P.lmax);
+    uint32_t *start = lsm + o.start, *cs = lsm + o.cs, *ve = lsm + o.ve, *ce = lsm + o.ce;
+    uint32_t *so = lsm + o.so, *rb = lsm + o.rb, *tend = lsm + o.tend, *lsl = lsm + o.lsl;
+    uint32_t *misc = lsm + o.misc, *tab = lsm + o.tab, *cb = lsm + o.cb, *ltag = lsm + o.ltag;
+    uint32_t *lgl = lsm + o.lgl;
+    uint32_t *stg = lsm + o.stg;
+    const uint32_t cap = 16u * P.lmax;   // the spare word
+    // list position x is "adjusted" a = x + ph: 64-byte lines are a >> 4
+    const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 15u);
+
+    // list starts (exclusive scan of totals); workgroup 0 also writes qstart
+    if (wave == 0) {
+        uint32_t carry = 0, nzb = 0;
+        for (uint32_t b0 = 0; b0 < nb; b0 += kWave) {
+            const uint32_t b = b0 + lane;
+            const uint32_t x0 = b < nb ? P.totals[b] : 0u;
+            nzb += (uint32_t)__popcll(__ballot(x0 != 0u));
+            const uint32_t x = wave_incl_scan(x0, lane);
+            if (b < nb) {
+                start[b] = carry + x - x0;
+                if (blockIdx.x == 0)
+                    P.qstart[b] = carry + x - x0;
+            }
+            carry += __shfl(x, kWave - 1, kWave);
+        }
+        if (lane == 0) {
+            if (blockIdx.x == 0)
+                P.qstart[nb] = carry;
+            misc[0] = nzb;
+            misc[3] = 0u;
+        }
+    }
+    __syncthreads();
+    if (misc[0] == 1u) {
+        // one non-empty list (all-UDP traffic): 0, 1, ..., n-1, grid-stride
+        // 16-byte non-temporal stores (64 MB in 10.7 us,
+        // profiles/r02_v8_hbm_write.log)
+        const uint32_t ph4 = ph & 3u;
+        const uint32_t head = min(P.n, (4u - ph4) & 3u);
+        const uint32_t nv = (P.n - head) >> 2;
+        const uint32_t T = gridDim.x * blockDim.x;
+        const uint32_t id = blockIdx.x * blockDim.x + t;
+        if (id < head)
+            P.qidx[id] = id;
+        u32x4 *dst = reinterpret_cast<u32x4 *>(P.qidx + head);
+        for (uint32_t v = id; v < nv; v += T) {
+            const uint32_t x = head + 4u * v;
+            __builtin_nontemporal_store(u32x4{x, x + 1u, x + 2u, x + 3u}, dst + v);
+        }
+        const uint32_t e = head + 4u * nv + id;
+        if (e < P.n)
+            P.qidx[e] = e;
+        return;
+    }
+
+    // this workgroup's range of spans
+    const uint32_t nsp = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
+    const uint32_t r = xcd_block(P.xcd), G = gridDim.x;
+    const uint32_t g0 = (uint32_t)((uint64_t)r * nsp / G);
+    const uint32_t g1 = (uint32_t)((uint64_t)(r + 1u) * nsp / G);
+    if (g0 >= g1)
+        return;
+    // prefix table rows are ncs + 1 words apart: with a power-of-two row the
+    // lanes of one chunk column hit one or two LDS banks whatever their bucket
+    // (a 0.78 conflict share of the LDS cycles at 64 buckets)
+    const uint32_t ncs = 1u << P.gshift, ntab = nb << P.gshift, rs = ncs + 1u;
+    auto prefix = [&](uint32_t b, uint32_t c) {
+        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : P.totals[b];
+    };
+    auto span_end = [&](uint32_t g) {
+        const uint64_t e = (uint64_t)g * P.seg + P.seg;
+        return e < P.n ? (uint32_t)e : P.n;
+    };
+    for (uint32_t b = t; b < nb; b += kLineBlock) {
+        const uint32_t a = start[b] + prefix(b, g0 << P.gshift) + ph;
+        cs[b] = a;
+        ve[b] = a;
+    }
+    u32x4 pk[kLineGroups], qk[kLineGroups];
+    uint32_t pt[kLineTabRegs], pend = 0;
+    auto load_span = [&](uint32_t g) {
+        const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
+        load_groups(P.rank, p0, pe, tt, pk);
+        if (!kPacked)
+            load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, qk);
+        const uint32_t c0 = g << P.gshift;
+        if (c0 + ncs < P.nchunk) {
+            // every column of the span and the next span's first are counts:
+            // element k * 512 + t is row (t >> gshift) + k * (512 >> gshift),
+            // column t & (ncs - 1), so one per-lane offset and a scalar step
+            // per k; rows past nb read 0 (range check)
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
+            const uint32_t vo = ((tt >> P.gshift) * P.ncol + (tt & (ncs - 1u))) * 4u;
+            const uint32_t step = (kLineBlock >> P.gshift) * P.ncol * 4u;
+#pragma unroll
+            for (uint32_t k = 0; k < kLineTabRegs; ++k)
+                pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, (int)(c0 * 4u + k * step), 0);
+            pend = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(tt * P.ncol * 4u),
+                                                        (int)((c0 + ncs) * 4u), 0);
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < kLineTabRegs; ++k) {
+                const uint32_t e = k * kLineBlock + tt;
+                pt[k] = e < ntab ? prefix(e >> P.gshift, c0 + (e & (ncs - 1u))) : 0u;
+            }
+            if (tt < nb)
+                pend = prefix(tt, c0 + ncs);
+        }
+    };
+    load_span(g0);
+    uint32_t wrote = 0;
+    for (uint32_t g = g0; g < g1; ++g) {
+        const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
+        const bool last = g + 1u == g1;
+        // (a) the span's prefixes: tab[b][c] at chunk c, tend[b] at its end
+#pragma unroll
+        for (uint32_t k = 0; k < kLineTabRegs; ++k) {
+            const uint32_t e = k * kLineBlock + t;
+            if (e < ntab)
+                tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k];
+        }
+        if (t < nb)
+            tend[t] = pend;
+        __syncthreads();
+        // (b) per bucket: the valid positions [cs, ve) = the carried words and
+        // the span's packets; its stage lines (exclusive scan), stage offset
+        // and the prefix rows' bias
+        if (wave == 0) {
+            uint32_t lines = 0;
+            for (uint32_t b0 = 0; b0 < nb; b0 += kWave) {
+                const uint32_t b = b0 + lane;
+                uint32_t nl = 0, v0 = 0, t0 = 0, e0 = 0;
+                if (b < nb) {
+                    e0 = ve[b];
+                    v0 = max(cs[b], e0 & ~15u);
+                    t0 = tab[b * rs];
+                    const uint32_t e1 = e0 + (tend[b] - t0);
+                    cs[b] = v0;
+                    ce[b] = e0;
+                    ve[b] = e1;
+                    nl = ((e1 + 15u) >> 4) - (v0 >> 4);
+                }
+                const uint32_t x = wave_incl_scan(nl, lane);
+                if (b < nb) {
+                    const uint32_t l0 = lines + x - nl;
+                    lsl[b] = l0;
+                    so[b] = 16u * (l0 - (v0 >> 4));
+                    rb[b] = 16u * (l0 - (v0 >> 4)) + e0 - t0;
+                }
+                lines += __shfl(x, kWave - 1, kWave);
+            }
+            if (lane == 0) {
+                if (lines > P.lmax) {
+                    report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g, lines);
+                    lines = 0;
+                }
+                lsl[nb] = lines;
+                misc[2] = lines;
+            }
+        }
+        __syncthreads();
+        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[2]);
+        // (c) prefix rows -> stage slots; stage pre-filled with the hole mark;
+        // each stage line tagged with its bucket, list line and copy mode
+        // (0 whole, 1 carried, 2 word by word)
+        for (uint32_t e = t; e < ntab; e += kLineBlock)
+            tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] += rb[e >> P.gshift];
+        for (uint32_t v = t; v < 4u * L; v += kLineBlock)
+            reinterpret_cast<u32x4 *>(stg)[v] = u32x4{kHole, kHole, kHole, kHole};
+        for (uint32_t l = t; l < L; l += kLineBlock) {
+            uint32_t lo = 0, hi = nb;   // lsl[lo] <= l < lsl[hi]
+            while (hi - lo > 1u) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (lsl[mid] <= l)
+                    lo = mid;
+                else
+                    hi = mid;
+            }
+            const uint32_t v0 = cs[lo], e1 = ve[lo], gl = l - lsl[lo] + (v0 >> 4);
+            const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
+                                  : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
+                                                                                  : 2u;
+            ltag[l] = lo | mode << 30;
+            lgl[l] = gl;
+        }
+        __syncthreads();
+        // (d) the carried words, then every packet at its slot
+        for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
+            const uint32_t b = e >> 4, j = e & 15u;
+            if (j < ce[b] - cs[b])
+                stg[min(so[b] + cs[b] + j, cap)] = cb[e];
+        }
+        // (a packed bucket past nb reads some other LDS word as its slot
+        // base: the slot is clamped and the hole it leaves is reported)
+        auto place = [&](auto ragged) {
+#pragma unroll
+            for (uint32_t k = 0; k < kLineGroups; ++k) {
+                const uint32_t o8 = 8u * (k * kLineBlock + t);
+                // chunks are multiples of 8 packets (clamped: groups past a short span)
+                const uint32_t cc = min(o8 >> P.cshift, ncs - 1u);
+                const uint32_t id = p0 + o8;
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j) {
+                    const uint32_t w = (pk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu;
+                    uint32_t b, rk;
+                    if (kPacked) {
+                        b = w >> P.cshift;
+                        rk = w & ((1u << P.cshift) - 1u);
+                    } else {
+                        b = bucket_of((int16_t)((qk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu),
+                                      P.nq);
+                        rk = w;
+                    }
+                    if (!decltype(ragged)::value || o8 + j < len)
+                        stg[min(tab[b * rs + cc] + rk, cap)] = id + j;
+                }
+            }
+        };
+        if (len == P.seg)
+            place(std::false_type{});
+        else
+            place(std::true_type{});
+        // the next span's streams and prefixes are in flight during the copy-out
+        if (!last)
+            load_span(g + 1u);
+        __syncthreads();
+        // (e) copy-out, a quad per thread: whole lines as 16-byte non-temporal
+        // stores; the bucket's last line, if the span ends inside it, is
+        // carried (unless the range ends here); partial lines word by word
+        for (uint32_t v = t; v < 4u * L; v += kLineBlock) {
+            const uint32_t l = v >> 2, tag = ltag[l], mode = tag >> 30;
+            const uint32_t a0 = 16u * lgl[l] + 4u * (v & 3u);
+            const u32x4 e = reinterpret_cast<const u32x4 *>(stg)[v];
+            if (mode == 0u) {
+                const bool hole = e.x == kHole || e.y == kHole || e.z == kHole || e.w == kHole;
+                const uint32_t d = a0 - ph;
+                if (!hole && d + 4u <= P.n && d + 4u > d) {
+                    __builtin_nontemporal_store(e, reinterpret_cast<u32x4 *>(P.qidx + d));
+                    wrote += 4u;
+                } else {
+                    report_fault(P.fault, hole ? YRSS_FAULT_STAGE : YRSS_FAULT_LIST_RANGE,
+                                 YRSS_K_SCATTER, g, d);
+                }
+            } else if (mode == 2u) {
+                const uint32_t b = tag & 0xffffu, v0 = cs[b], e1 = ve[b];
+#pragma unroll
+                for (uint32_t j = 0; j < 4u; ++j) {
+                    const uint32_t a = a0 + j;
+                    if (a < v0 || a >= e1)
+                        continue;
+                    const uint32_t w = e[j], d = a - ph;
+                    if (w != kHole && d < P.n) {
+                        P.qidx[d] = w;
+                        ++wrote;
+                    } else {
+                        report_fault(P.fault, w == kHole ? YRSS_FAULT_STAGE : YRSS_FAULT_LIST_RANGE,
+                                     YRSS_K_SCATTER, g, d);
+                    }
+                }
+            }
+        }
+        // (f) carry the unfinished last lines
+        if (!last) {
+            for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
+                const uint32_t b = e >> 4, j = e & 15u;
+                const uint32_t e1 = ve[b], nv = max(cs[b], e1 & ~15u);
+                if (j < e1 - nv)
+                    cb[e] = stg[min(so[b] + nv + j, cap)];
+            }
+        }
+    }
+    // every packet of the range left exactly once
+    wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
+    if (lane == 0)
+        atomicAdd(&misc[3], wrote);
+    __syncthreads();
+    if (t == 0) {
+        const uint32_t want = span_end(g1 - 1u) - g0 * P.seg;
+        if (misc[3] != want)
+            report_fault(P.fault, YRSS_FAULT_COUNT_MISMATCH, YRSS_K_SCATTER, g0, misc[3]);
     }
 }
 
@@ -2251,6 +2655,43 @@ ScatterLds scatter_lds(uint32_t nb, const Layout &lay)
     return r;
 }
 
+// The line scatter's span and stage for a layout: spans of up to
+// kLineSpanMax packets (yrss_tuning.span_tiles lowers it), as many chunks as
+// keep the prefix table within kLineTabMax words; none when a chunk is longer
+// than a span can be (batches past ~2^29 packets) or the LDS would not fit.
+struct LinePlan {
+    bool ok, packed;
+    uint32_t gshift, seg, lmax, lds;
+};
+
+LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
+{
+    LinePlan p{};
+    const uint32_t nb = c->nb, cshift = lay.ct_shift + 6u;
+    if (lay.chunk > kLineSpanMax || nb > (uint32_t)kLineBlock)
+        return p;
+    uint64_t target = c->tune.span_tiles ? (uint64_t)c->tune.span_tiles * kTile : kLineSpanMax;
+    target = std::min<uint64_t>(std::max<uint64_t>(target, lay.chunk), kLineSpanMax);
+    p.gshift = 0;
+    while (((uint64_t)lay.chunk << (p.gshift + 1)) <= target &&
+           ((uint64_t)nb << (p.gshift + 1)) <= kLineTabMax)
+        ++p.gshift;
+    if (((uint64_t)nb << p.gshift) > kLineTabMax)
+        return p;
+    p.seg = lay.chunk << p.gshift;
+    p.lmax = p.seg / 16u + 2u * nb + 1u;   // a bucket's lines <= (its packets + 30) / 16
+    p.lds = line_lds(nb, p.gshift, p.lmax).words * 4u;
+    if (p.lds > 160u * 1024u)
+        return p;
+    // bucket << cshift | rank fits 16 bits
+    p.packed = cshift < 16u && nb <= (1u << (16u - cshift));
+#ifdef YRSS_AB_NOPACK
+    p.packed = false;
+#endif
+    p.ok = true;
+    return p;
+}
+
 // Workgroups of kernel fn (block threads, lds bytes) resident on the whole
 // device at once, from the occupancy calculator, cached per context.
 uint32_t resident_blocks(yrss_ctx *c, const void *fn, uint32_t block, uint32_t lds)
@@ -3001,8 +3442,10 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     if (compact && ((uint64_t)lay.nchunk + pwaves - 1) / pwaves * c->nb > kCntWords)
         return -EINVAL;   // layout_for sizes chunks so a wave's count slots fit
     const ScatterLds sl = scatter_lds(c->nb, lay);
-    // the ranked scatter reads q as 16-byte vectors
-    const bool ranked = compact && sl.ranked && ((uintptr_t)b->q & 15u) == 0;
+    const LinePlan lp = line_plan(c, lay);
+    // the line scatter reads q (when the bucket is not packed with the rank)
+    // as 16-byte vectors
+    const bool ranked = compact && lp.ok && (lp.packed || ((uintptr_t)b->q & 15u) == 0);
     if (ranked && c->rank_cap < n) {
         // the ranks' workspace grows to the largest batch seen; the old one
         // may still be read by a scatter queued on this stream
@@ -3032,6 +3475,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     P.filter = b->filter;
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
+    P.rank_pack = ranked && lp.packed ? 1u : 0u;
     {
         Timed t(c, YRSS_K_PARSE_HASH);
         hipExtLaunchKernelGGL(pick_parse(ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
@@ -3059,6 +3503,37 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
                               t.a, t.b, 0, SP);
     }
     YRSS_HIP(hipGetLastError());
+    if (ranked) {
+        LineParams S;
+        S.q = b->q;
+        S.rank = c->d_rank;
+        S.seg_off = c->d_seg_off;
+        S.totals = c->d_totals;
+        S.qidx = b->qidx;
+        S.qstart = b->qstart;
+        S.fault = c->d_fault_rec;
+        S.n = n;
+        S.nq = c->cfg.nb_queues;
+        S.nb = c->nb;
+        S.nchunk = lay.nchunk;
+        S.ncol = lay.ncol;
+        S.seg = lp.seg;
+        S.gshift = lp.gshift;
+        S.cshift = lay.ct_shift + 6u;
+        S.lmax = lp.lmax;
+        S.xcd = c->tune.scatter_xcd != 0 ? 1u : 0u;
+        // persistent: the resident workgroups, each one contiguous range of
+        // spans, never more workgroups than spans
+        const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
+        void (*fn)(LineParams) = lp.packed ? yrss_scatter_lines<true> : yrss_scatter_lines<false>;
+        const uint32_t sgrid =
+            std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
+        Timed t(c, YRSS_K_SCATTER);
+        hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(kLineBlock), lp.lds, s, t.a,
+                              t.b, 0, S);
+        YRSS_HIP(hipGetLastError());
+        return 0;
+    }
     ScatterParams S;
     S.q = b->q;
     S.seg_off = c->d_seg_off;
