@@ -1,13 +1,22 @@
 """Parity across the work layouts and scatter paths (GPU).
 
-The parse kernel deals chunks of tiles round-robin to its waves and counts per
-chunk; the scatter ranks and stages each span of chunks itself (yrss.hip
-layout_for, yrss_scatter).  Chunk size, span size, parse grid and the
-XCD-contiguous span mapping are layout choices only (yrss_set_tuning): every
-combination, with the fused protocol_filter on or off, ragged batch sizes and
-window strides 64 and 80, must give the oracle's q, hash and per-queue FIFO
-lists bit-exactly (fs/lib/ff_dpdk_if.c:1945-2113 and the process_packets
-enqueue order, :1058-1094), and no device guard may fire (fault record empty).
+The parse kernel deals chunks of tiles round-robin to its waves, counts per
+chunk and ranks every packet in its chunk; the line scatter places each span
+of chunks by those ranks (packed beside the bucket when it fits, else read
+beside q) and writes whole list lines, carrying a bucket's unfinished line to
+the next span; chunks longer than a span take the fallback scatter, which
+ranks from q itself (yrss.hip layout_for, line_plan, yrss_scatter_lines,
+yrss_scatter).  Chunk size, span size, parse grid and the XCD-contiguous
+range mapping are layout choices only (yrss_set_tuning): every combination,
+with the fused protocol_filter on or off, ragged batch sizes and window
+strides 64 and 80, must give the oracle's q, hash and per-queue FIFO lists
+bit-exactly (fs/lib/ff_dpdk_if.c:1945-2113 and the process_packets enqueue
+order, :1058-1094), and no device guard may fire (fault record empty).
+
+Paths and how the tests reach them: line scatter packed (<= 128 buckets at
+default chunks), line scatter with q (257 buckets: 16-tile chunks leave no
+room beside the rank), fallback (chunk_tiles=256: a chunk past the 8192-packet
+span), one list (all-UDP), each with filter on and off.
 """
 import numpy as np
 import pytest
@@ -64,11 +73,12 @@ def check(eng, oracle_mod, cfg_tuple, profile, n, stride=64, first=0, want_filte
 
 @pytest.mark.parametrize("want_filter", [False, True])
 @pytest.mark.parametrize("chunk,span", [(1, 1), (1, 64), (2, 2), (8, 64), (32, 32),
-                                        (4, 256), (128, 128)])
+                                        (4, 256), (128, 128), (256, 256)])
 @pytest.mark.parametrize("profile", [abi.SYN_TCP4, abi.SYN_FUZZ])
 def test_forced_layouts(dev, oracle_mod, chunk, span, profile, want_filter):
     """Chunk and span sizes are layout choices only: results never change
-    (spans of several pieces and spans of a fraction of a chunk included)."""
+    (one-chunk spans, spans shorter than requested, and chunks past the line
+    scatter's span, which take the fallback scatter, included)."""
     cfg = (5, 5, 1, 1)
     with SoftRss(*cfg, device=0, max_burst=0) as eng:
         eng.set_tuning(chunk_tiles=chunk, span_tiles=span)

@@ -234,6 +234,7 @@ _PROTOS = {
 }
 
 _lib = None
+_libs: dict[str, ctypes.CDLL] = {}
 
 
 def header_functions(path: Path = HEADER_PATH) -> list[str]:
@@ -245,25 +246,33 @@ def header_functions(path: Path = HEADER_PATH) -> list[str]:
     return sorted(set(names))
 
 
-def load() -> ctypes.CDLL:
-    """Load libyrss.so (once).  Raises YrssLibraryError if it is absent."""
+def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
+    """Load libyrss.so (once per path; default YRSS_LIB or the in-tree build).
+    Raises YrssLibraryError if it is absent.  Distinct paths load side by side
+    (RTLD_LOCAL), which tools/ab_inproc.py uses to compare builds in one
+    process."""
     global _lib
-    if _lib is not None:
+    if path is None and _lib is not None:
         return _lib
-    path = Path(os.environ.get("YRSS_LIB", LIB_PATH))
-    if not path.exists():
+    p = Path(path if path is not None else os.environ.get("YRSS_LIB", LIB_PATH))
+    key = str(p.resolve()) if p.exists() else str(p)
+    if key in _libs:
+        return _libs[key]
+    if not p.exists():
         raise YrssLibraryError(
-            f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
         )
     try:
-        lib = ctypes.CDLL(str(path))
+        lib = ctypes.CDLL(str(p))
     except OSError as e:  # pragma: no cover - environment specific
-        raise YrssLibraryError(f"cannot load {path}: {e}") from e
+        raise YrssLibraryError(f"cannot load {p}: {e}") from e
     for name, (res, args) in _PROTOS.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    _libs[key] = lib
+    if path is None:
+        _lib = lib
     return lib
 
 

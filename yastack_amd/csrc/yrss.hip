@@ -54,9 +54,8 @@ constexpr int kScatterWaves = kScatterBlock / kWave;
 constexpr uint32_t kMaxChunks = 65536;  // per launch; bounds the count matrix [nb][ncol]
 constexpr uint32_t kCntWords = 2176;    // parse: per-wave LDS count slots (chunks x nb): 32 x 68
 constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
-constexpr uint32_t kPiece = 2048;       // scatter: packets ranked and staged at once per wave
+constexpr uint32_t kPiece = 2048;       // fallback scatter: packets ranked and staged at once per wave
 constexpr uint32_t kPieceSlots = kPiece / 64;   // 64-packet slots of a piece
-constexpr uint32_t kTab = 17;           // ranked scatter: prefix-table words per lane (nb x 2nc <= 1088)
 // Toeplitz key tables: the 96 tuple bits are cut into 12 bytes (MSB first);
 // table t maps a byte value to the XOR of the key windows its set bits select
 // (12 lookups per hash).  Nibble tables (24 conflict-free lookups) and
@@ -114,7 +113,6 @@ struct ScatterParams {
     uint32_t ncol;             // row stride of seg_off
     uint32_t gshift;           // a span is 2^gshift chunks
     uint32_t cshift;           // a chunk is 2^cshift packets
-    const uint16_t *rank;      // ranked mode: rank in chunk per packet (parse kCount == 2)
     uint32_t aux;              // words of a wave's per-bucket arrays ahead of its stage
     uint32_t stg;              // words of a wave's stage (kPiece + 3 per bucket, rounded)
     uint32_t wlds;             // words of LDS per wave
@@ -339,10 +337,17 @@ __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc(
         P.hash ? (void *)(P.hash + t_first) : (void *)P.q, 0, P.hash ? (int)(nv * 4u) : 0,
         kRsrcWord3);
-    if (P.out16 && nv == ntiles * (uint32_t)kTile) {
+    constexpr bool kRankWide = true;
+    const bool wide = P.out16 && nv == ntiles * (uint32_t)kTile;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        kRank ? (void *)(P.rank + t_first) : (void *)P.q, 0, kRank ? (int)(nv * 2u) : 0,
+        kRsrcWord3);
+    if (wide) {
         // a whole batch of tiles: 16-byte write-through (sc1) stores, 1 KiB of
-        // hash and 512 B of q per wave-instruction at 4 tiles; the lines leave
-        // L2 at once, none is left dirty at kernel end
+        // hash and 512 B of q (and of ranks) per wave-instruction at 4 tiles;
+        // the lines leave L2 at once, none is left dirty at kernel end (plain
+        // rank stores left 32 MB of dirty lines in L2, written back inside the
+        // next parse kernel: +7 us there, r03 A/B)
         wave_lds_sync();
         const uint32_t nh = nv >> 2, nq8 = nv >> 3;
         const u32x4 vh = *reinterpret_cast<const u32x4 *>(oh + 4u * min(lane, nh - 1u));
@@ -351,6 +356,11 @@ __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *
             __builtin_amdgcn_raw_buffer_store_b128(vh, rh, (int)(lane * 16u), 0, 16);
         if (lane < nq8)
             __builtin_amdgcn_raw_buffer_store_b128(vq, rq, (int)(lane * 16u), 0, 16);
+        if (kRank && kRankWide) {
+            const u32x4 vr = *reinterpret_cast<const u32x4 *>(orank + 8u * min(lane, nq8 - 1u));
+            if (lane < nq8)
+                __builtin_amdgcn_raw_buffer_store_b128(vr, rr, (int)(lane * 16u), 0, 16);
+        }
         wave_lds_sync();
     } else {
         for (uint32_t j = 0; j < ntiles; ++j) {
@@ -367,9 +377,7 @@ __device__ __forceinline__ void flush_out(const ParseParams &P, const uint16_t *
             __builtin_amdgcn_raw_buffer_store_b8((uint8_t)of[e], rf, (int)e, 0, 0);
         }
     }
-    if (kRank) {
-        const __amdgpu_buffer_rsrc_t rr =
-            __builtin_amdgcn_make_buffer_rsrc(P.rank + t_first, 0, (int)(nv * 2u), kRsrcWord3);
+    if (kRank && !(wide && kRankWide)) {
         for (uint32_t j = 0; j < ntiles; ++j) {
             const uint32_t e = j * kTile + lane;
             __builtin_amdgcn_raw_buffer_store_b16(orank[e], rr, (int)(e * 2u), 0, 0);
@@ -777,17 +785,53 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
     reinterpret_cast<uint4 *>(P.off + (size_t)b * P.ncol)[col / 4u] = o;
 }
 
+// List stores are streaming and written through at device scope (nt | sc1):
+// with non-temporal stores alone the lines stayed dirty past the scatter and
+// their write-back landed in the next batch's parse kernel (+19 us there at 9
+// buckets, same-process A/B, profiles/r03_ab_inproc_store.log).
+constexpr int kListAux = 18;   // nt | sc1
+
+// The lists as a buffer resource: offsets are 32-bit, so lists past 2^29
+// entries take flat non-temporal stores instead (wide = false).
+struct ListOut {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t *p;
+    bool wide;
+};
+__device__ __forceinline__ ListOut list_out(uint32_t *qidx, uint32_t n)
+{
+    const bool wide = n < (1u << 29);
+    return ListOut{__builtin_amdgcn_make_buffer_rsrc(qidx, 0, wide ? (int)(n * 4u) : 0, kRsrcWord3),
+                   qidx, wide};
+}
+template <int kAux>
+__device__ __forceinline__ void list_store4(const ListOut &o, uint32_t d, u32x4 v)
+{
+    if (o.wide)
+        __builtin_amdgcn_raw_buffer_store_b128(v, o.r, (int)(d * 4u), 0, kAux);
+    else
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(o.p + d));
+}
+template <int kAux>
+__device__ __forceinline__ void list_store1(const ListOut &o, uint32_t d, uint32_t v)
+{
+    if (o.wide)
+        __builtin_amdgcn_raw_buffer_store_b32(v, o.r, (int)(d * 4u), 0, kAux);
+    else
+        o.p[d] = v;
+}
+
 // ---------------------------------------------------------------------------
-// Kernel 3: stable scatter of packet indices into the per-bucket lists: the
-// FIFO rte_ring_enqueue into dispatch_ring[port][q] of process_packets
-// (ff_dpdk_if.c:1087-1093), for a whole batch.
+// Kernel 3b: the lists when a parse chunk is longer than the line scatter's
+// span (batches past ~2^29 packets): the stable scatter of packet indices into
+// the per-bucket lists, the FIFO rte_ring_enqueue into dispatch_ring[port][q]
+// of process_packets (ff_dpdk_if.c:1087-1093), ranking from q itself.
 //
 // Persistent: as many waves as are resident, wave w taking spans w, w + W, ...
-// (a span is 2^gshift parse chunks, 2048 packets by default), so the waves in
-// flight together cover one stretch of the batch.  A span's lists start at
-// its buckets' prefixes from the scan (start[b] + prefix[b][first chunk]).
-// The span is worked in pieces of up to kPiece packets, each in three steps
-// that touch only LDS and registers:
+// (a span is 2^gshift parse chunks), so the waves in flight together cover one
+// stretch of the batch.  A span's lists start at its buckets' prefixes from the
+// scan (start[b] + prefix[b][first chunk]).  The span is worked in pieces of
+// up to kPiece packets, each in three steps that touch only LDS and registers:
 //   count  the piece's q (loaded slot-major, 32 x 64 packets, one piece ahead)
 //          is histogrammed per bucket: lanes sharing a bucket are found with
 //          ceil(log2 nb) ballots, the lowest adds the group's size;
@@ -798,18 +842,13 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
 //   copy   the stage is written out in order.  A bucket's run starts at a
 //          stage slot congruent to its list position mod 4 (at most 3 words
 //          of padding per bucket), so four stage words that share a bucket
-//          are one aligned 16-byte store; quads in lines the piece writes
-//          whole go out non-temporal, the rest plain (L2 merges a line's
-//          pieces: non-temporal partial lines cost 1.6x,
-//          profiles/r01_v5_scatter_sweep.log).
-// The scatter ranks packets itself from q: the parse kernel only counts per
-// chunk (the scan turns that into the spans' list offsets), and a span's own
-// histogram is checked against those counts at its end.  Any disagreement, and
-// any destination outside the batch, is reported through the fault record
-// instead of stored (YRSS_FAULT_COUNT_MISMATCH / _LIST_RANGE / _STAGE).
-// A batch whose totals show one non-empty list (all-UDP traffic, the headline
-// config) takes the identity path: its list is 0, 1, ..., n-1, written
-// grid-stride as 16-byte non-temporal stores without reading q.
+//          are one aligned 16-byte store, the rest word by word.
+// A span's histogram is checked against the parse kernel's counts at its end.
+// Any disagreement, and any destination outside the batch, is reported
+// through the fault record instead of stored (YRSS_FAULT_COUNT_MISMATCH /
+// _LIST_RANGE / _STAGE).  Ranking in the scatter costs ~70 VALU per 64
+// packets (ballots, twice), against ~13 for placing by the parse kernel's
+// ranks, so this is the large-batch path only (yrss_scatter_lines otherwise).
 // ---------------------------------------------------------------------------
 
 // The piece's q (or ranks), slot-major (slot s, lane l -> packet p0 + 64 s +
@@ -886,35 +925,12 @@ __device__ __forceinline__ void rank_piece(const ScatterParams &P,
 // Writes a piece's stage out, quad by quad: four words of one bucket are one
 // aligned 16-byte store (non-temporal when the piece writes the whole line),
 // others word by word.  Returns how many entries this lane wrote.
-#ifndef YRSS_AB_STORE
-#define YRSS_AB_STORE 0
-#endif
 __device__ __forceinline__ uint32_t copy_out(const ScatterParams &P, const uint32_t *stg,
                                              const uint32_t *base, const uint32_t *ls,
                                              const uint32_t *cnt, uint32_t p0, uint32_t ph,
                                              uint32_t lane)
 {
     uint32_t wrote = 0;
-#if YRSS_AB_STORE == 5 || YRSS_AB_STORE == 6
-    for (uint32_t k = lane; k < P.stg; k += kWave) {
-        const uint32_t w = stg[k], bk = w & 511u;
-        if (bk >= P.nb)
-            continue;
-        const uint32_t kk = k - ls[bk], d = base[bk] + kk;
-        if (kk < cnt[bk] && d < P.n) {
-#if YRSS_AB_STORE == 5
-            __builtin_nontemporal_store(p0 + (w >> 9), P.qidx + d);
-#else
-            P.qidx[d] = p0 + (w >> 9);
-#endif
-            ++wrote;
-        } else {
-            report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, p0 + (w >> 9), d);
-        }
-    }
-    (void)ph;
-    return wrote;
-#endif
     for (uint32_t v = lane; v < P.stg / 4u; v += kWave) {
         const u32x4 e = reinterpret_cast<const u32x4 *>(stg)[v];
         const uint32_t b = e.x & 511u;
@@ -945,11 +961,7 @@ __device__ __forceinline__ uint32_t copy_out(const ScatterParams &P, const uint3
                 const uint32_t kk = 4u * v + k - ls[bk];
                 const uint32_t d = base[bk] + kk;
                 if (kk < cnt[bk] && d < P.n) {
-#if YRSS_AB_STORE == 4
-                    __builtin_nontemporal_store(p0 + (w >> 9), P.qidx + d);
-#else
                     P.qidx[d] = p0 + (w >> 9);
-#endif
                     ++wrote;
                 } else {
                     report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, p0 + (w >> 9),
@@ -965,45 +977,6 @@ __device__ __forceinline__ uint32_t copy_out(const ScatterParams &P, const uint3
     return wrote;
 }
 
-// A piece's 2048 16-bit words, lane-major: register k of lane l holds words
-// 8 (64 k + l) .. + 7 (four 16-byte loads a lane, the values come packed).
-// The base must be 16-byte aligned; words past pe read 0 (range check).
-__device__ __forceinline__ void load_piece16(const uint16_t *a, uint32_t p0, uint32_t pe,
-                                             uint32_t lane, u32x4 (&v)[kPiece / 512])
-{
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t *>(a + p0), 0, (int)((pe - p0) * 2u), kRsrcWord3);
-    if (((pe - p0) & 7u) == 0) {
-#pragma unroll
-        for (uint32_t k = 0; k < kPiece / 512; ++k)
-            v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 r, (int)((k * 64u + lane) * 16u), 0, 2 /* nt */));
-    } else {
-        // the batch's last piece ends inside a 16-byte vector, which the range
-        // check would drop whole: word by word
-#pragma unroll
-        for (uint32_t k = 0; k < kPiece / 512; ++k) {
-            uint32_t w[4];
-#pragma unroll
-            for (uint32_t i = 0; i < 4u; ++i) {
-                const int o = (int)((k * 64u + lane) * 16u + 4u * i);
-                w[i] = __builtin_amdgcn_raw_buffer_load_b16(r, o, 0, 0) |
-                       ((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, o + 2, 0, 0) << 16);
-            }
-            v[k] = u32x4{w[0], w[1], w[2], w[3]};
-        }
-    }
-}
-
-// kRanked: the parse kernel wrote each packet's rank in its chunk and a span
-// (one piece) is a whole number of chunks, so a packet's stage slot is
-// off[chunk][bucket] + rank with off from the scan's prefixes: about 13 VALU
-// per 64 packets, where ranking in the scatter (ballot match per slot, twice:
-// histogram then placement) cost ~70 and made the kernel VALU-bound (62-198
-// us against 23-65 at 4-256 buckets, profiles/r03_v1_qrows.log).  !kRanked
-// (chunks longer than a piece: batches past ~2^26 packets with many buckets)
-// ranks in the scatter, piece by piece.
-template <bool kRanked>
 __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1012,9 +985,8 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
     const uint32_t wpb = blockDim.x / kWave;
     // per wave: start[nb] the lists' starts; base[nb] the piece's first list
     // slot per bucket; ls[nb] the bucket's run start in the stage; cnt[nb]
-    // the piece's count per bucket; then (ranked) off[chunks][nb], the
-    // placement offsets, or (self-ranked) cur[nb] the placement cursors and
-    // send[nb] the span's end per bucket; then the stage
+    // the piece's count per bucket; cur[nb] the placement cursors; send[nb]
+    // the span's end per bucket; then the stage
     uint32_t *start = reinterpret_cast<uint32_t *>(smem) + wave * P.wlds;
     uint32_t *base = start + P.nb, *ls = base + P.nb, *cnt = ls + P.nb;
     uint32_t *cur = cnt + P.nb, *send = cur + P.nb;
@@ -1042,25 +1014,22 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
     }
     if (gw == 0 && lane == 0)
         P.qstart[P.nb] = carry;
+    const ListOut lout = list_out(P.qidx, P.n);
     if (nzb == 1) {
         // one non-empty list (all-UDP traffic): 0, 1, ..., n-1, grid-stride
-        // 16-byte non-temporal stores, the layout that writes fastest (64 MB
-        // in 10.7 us against 11.9 us for one group per wave,
-        // profiles/r02_v8_hbm_write.log)
         const uint32_t head = min(P.n, (4u - ph) & 3u);
         const uint32_t nv = (P.n - head) >> 2;
         const uint32_t T = gridDim.x * blockDim.x;
         const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
         if (id < head)
-            P.qidx[id] = id;
-        u32x4 *dst = reinterpret_cast<u32x4 *>(P.qidx + head);
+            list_store1<kListAux>(lout, id, id);
         for (uint32_t v = id; v < nv; v += T) {
             const uint32_t x = head + 4u * v;
-            __builtin_nontemporal_store(u32x4{x, x + 1u, x + 2u, x + 3u}, dst + v);
+            list_store4<kListAux>(lout, x, u32x4{x, x + 1u, x + 2u, x + 3u});
         }
         const uint32_t t = head + 4u * nv + id;
         if (t < P.n)
-            P.qidx[t] = t;
+            list_store1<kListAux>(lout, t, t);
         return;
     }
     if (gw >= ng)
@@ -1091,98 +1060,7 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
     };
     wave_lds_sync();
 
-    if constexpr (kRanked) {
-        // tab[b][c], c = 0..nc: the bucket's prefix at the span's chunk c
-        // (c = nc: the next span's first chunk), ncp = 2nc words per bucket;
-        // loaded one span ahead with the q and ranks (kTab words per lane:
-        // layout_for keeps nb x ncp <= 64 kTab), then turned in place into
-        // the placement offsets off[b][c] = ls[b] + the bucket's packets in
-        // the span's chunks before c
-        const uint32_t nc = 1u << P.gshift;   // chunks per span (one piece)
-        const uint32_t lcp = P.gshift + 1u, ntab = P.nb << lcp;
-        uint32_t *tab = cnt + P.nb;
-        u32x4 qp[kPiece / 512], rp[kPiece / 512];
-        uint32_t pt[kTab];
-        auto load_tab = [&](uint32_t g) {
-            const uint32_t c0 = g << P.gshift, ln = opaque(lane);
-#pragma unroll
-            for (uint32_t k = 0; k < kTab; ++k) {
-                const uint32_t e = k * 64u + ln;
-                const uint32_t b = min(e >> lcp, P.nb - 1u), c = min(e & ((2u << P.gshift) - 1u), nc);
-                pt[k] = prefix(b, c0 + c);
-            }
-        };
-        uint32_t g = gw;
-        uint32_t p0 = g * P.seg, pe = span_end(g);
-        load_piece16(reinterpret_cast<const uint16_t *>(P.q), p0, pe, opaque(lane), qp);
-        load_piece16(P.rank, p0, pe, opaque(lane), rp);
-        load_tab(g);
-        for (;;) {
-#pragma unroll
-            for (uint32_t k = 0; k < kTab; ++k)
-                if (k * 64u + lane < ntab)
-                    tab[k * 64u + lane] = pt[k];
-            wave_lds_sync();
-            for (uint32_t b = lane; b < P.nb; b += kWave) {
-                const uint32_t o0 = tab[b << lcp];
-                base[b] = start[b] + o0;
-                cnt[b] = tab[(b << lcp) + nc] - o0;
-            }
-            wave_lds_sync();
-            layout();
-            wave_lds_sync();
-            // off = ls[b] + prefix - prefix at the span's first chunk (=
-            // base[b] - start[b]), every entry in parallel
-            for (uint32_t e = lane; e < ntab; e += kWave) {
-                const uint32_t b = e >> lcp;
-                tab[e] = ls[b] + tab[e] - (base[b] - start[b]);
-            }
-            wave_lds_sync();
-            // place: stage slot = off[bucket][chunk] + rank, entry (packet -
-            // p0) << 9 | bucket; lanes past the span's end store into the
-            // spare word after the stage.  No branch per slot: the copy-out
-            // checks every entry against its bucket's run and counts them.
-            // packet o = 8 (64 k + lane) + j; chunks are multiples of 8
-            // packets, so its chunk is (512 k + 8 lane) >> cshift for every j
-            const uint32_t len = pe - p0, ln = opaque(lane);
-#pragma unroll
-            for (uint32_t k = 0; k < kPiece / 512; ++k) {
-                const uint32_t o8 = (k * 64u + ln) * 8u;
-                const uint32_t *tk = tab + (o8 >> P.cshift);
-#pragma unroll
-                for (uint32_t j = 0; j < 8u; ++j) {
-                    const uint32_t w = j >> 1, sh = 16u * (j & 1u);
-                    const uint32_t b = bucket_of((int16_t)((qp[k][w] >> sh) & 0xffffu), P.nq);
-                    const uint32_t r = (rp[k][w] >> sh) & 0xffffu;
-                    const uint32_t slot = min(tk[b << lcp] + r, P.stg);
-                    stg[o8 + j < len ? slot : P.stg] = ((o8 + j) << 9) | b;
-                }
-            }
-            // the next span's q, ranks and prefixes are in flight during the
-            // copy-out
-            const uint32_t g2 = g + W;
-            const bool more = g2 < ng;
-            const uint32_t p2 = more ? g2 * P.seg : 0u, pe2 = more ? span_end(g2) : 0u;
-            if (more) {
-                load_piece16(reinterpret_cast<const uint16_t *>(P.q), p2, pe2, opaque(lane), qp);
-                load_piece16(P.rank, p2, pe2, opaque(lane), rp);
-                load_tab(g2);
-            }
-            wave_lds_sync();
-            uint32_t wrote = copy_out(P, stg, base, ls, cnt, p0, ph, lane);
-            // every packet of the span left exactly once: two packets on one
-            // slot would leave a hole (padding) inside a run
-            wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
-            if (lane == 0 && wrote != pe - p0)
-                report_fault(P.fault, YRSS_FAULT_COUNT_MISMATCH, YRSS_K_SCATTER, g, wrote);
-            wave_lds_sync();
-            if (!more)
-                break;
-            g = g2;
-            p0 = p2;
-            pe = pe2;
-        }
-    } else {
+    {
         uint32_t g = gw, p0 = gw * P.seg;
         uint32_t pe = min(span_end(g), p0 + kPiece);
         uint32_t qv[kPieceSlots], qn[kPieceSlots];
@@ -1245,7 +1123,7 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
 // Kernel 3 (ranked): the lists written in whole 64-byte lines.
 //
 // A workgroup takes one contiguous range of spans (a span: 2^gshift parse
-// chunks, up to kLineSpanMax packets) and works them in order.  Per span it
+// chunks, up to line_span_max(kG) packets) and works them in order.  Per span it
 // places every packet in an LDS stage by the parse kernel's rank (stage slot =
 // the bucket's position for its chunk + rank, the positions from the scan's
 // prefixes), the stage laid out line for line like the lists: bucket b's
@@ -1270,11 +1148,15 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
 // storing (YRSS_FAULT_STAGE / _LIST_RANGE / _COUNT_MISMATCH).
 // ---------------------------------------------------------------------------
 constexpr int kLineBlock = 512;
-constexpr uint32_t kLineGroups = 2;                                 // 8-packet groups a thread
-constexpr uint32_t kLineSpanMax = kLineBlock * 8u * kLineGroups;   // 8192 packets
-constexpr uint32_t kLineTabRegs = 8;                                // prefix words a thread
-constexpr uint32_t kLineTabMax = kLineBlock * kLineTabRegs;        // nb x span chunks <= 4096
+constexpr uint32_t kLineTabRegs = 9;                     // prefix words a thread
+constexpr uint32_t kLineTabMax = kLineBlock * kLineTabRegs;  // nb x span chunks <= 4608
+// A span is kG 8-packet groups a thread: 8192 packets (kG = 2) up to 128
+// buckets, 16384 (kG = 4) past that, where the per-bucket work of a span
+// (carried lines, layout) is large enough to amortise over twice the packets
+// (q255 scatter 93 -> 75 us; at 64 buckets kG = 4 cost 3-4 us, r03 A/B).
+constexpr uint32_t line_span_max(uint32_t g) { return kLineBlock * 8u * g; }
 constexpr uint32_t kHole = 0xFFFFFFFFu;
+
 
 struct LineParams {
     const int16_t *q;          // !kPacked: the bucket of each packet
@@ -1285,7 +1167,7 @@ struct LineParams {
     uint32_t *qstart;          // [nb + 1]
     uint32_t *fault;
     uint32_t n, nq, nb, nchunk, ncol;
-    uint32_t seg;              // packets per span: 2^gshift chunks, <= kLineSpanMax
+    uint32_t seg;              // packets per span: 2^gshift chunks, <= line_span_max(kG)
     uint32_t gshift, cshift;   // span = 2^gshift chunks, chunk = 2^cshift packets
     uint32_t lmax;             // stage lines: seg / 16 + 2 nb + 1
     uint32_t xcd;              // workgroups of one XCD take consecutive ranges
@@ -1327,19 +1209,20 @@ __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32
 // p0 + 8 (512 k + t) ..+7; past pe read 0 (range check; a batch's last span
 // that ends inside a vector is read word by word, as the check drops a
 // partial vector whole).
+template <uint32_t kG>
 __device__ __forceinline__ void load_groups(const uint16_t *a, uint32_t p0, uint32_t pe,
-                                            uint32_t t, u32x4 (&v)[kLineGroups])
+                                            uint32_t t, u32x4 (&v)[kG])
 {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint16_t *>(a + p0), 0, (int)((pe - p0) * 2u), kRsrcWord3);
     if (((pe - p0) & 7u) == 0) {
 #pragma unroll
-        for (uint32_t k = 0; k < kLineGroups; ++k)
+        for (uint32_t k = 0; k < kG; ++k)
             v[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                  r, (int)((k * kLineBlock + t) * 16u), 0, 2));
     } else {
 #pragma unroll
-        for (uint32_t k = 0; k < kLineGroups; ++k) {
+        for (uint32_t k = 0; k < kG; ++k) {
             uint32_t w[4];
 #pragma unroll
             for (uint32_t i = 0; i < 4u; ++i) {
@@ -1352,7 +1235,7 @@ __device__ __forceinline__ void load_groups(const uint16_t *a, uint32_t p0, uint
     }
 }
 
-template <bool kPacked>
+template <bool kPacked, uint32_t kG>
 __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
@@ -1395,21 +1278,21 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         // one non-empty list (all-UDP traffic): 0, 1, ..., n-1, grid-stride
         // 16-byte non-temporal stores (64 MB in 10.7 us,
         // profiles/r02_v8_hbm_write.log)
+        const ListOut lo = list_out(P.qidx, P.n);
         const uint32_t ph4 = ph & 3u;
         const uint32_t head = min(P.n, (4u - ph4) & 3u);
         const uint32_t nv = (P.n - head) >> 2;
         const uint32_t T = gridDim.x * blockDim.x;
         const uint32_t id = blockIdx.x * blockDim.x + t;
         if (id < head)
-            P.qidx[id] = id;
-        u32x4 *dst = reinterpret_cast<u32x4 *>(P.qidx + head);
+            list_store1<kListAux>(lo, id, id);
         for (uint32_t v = id; v < nv; v += T) {
             const uint32_t x = head + 4u * v;
-            __builtin_nontemporal_store(u32x4{x, x + 1u, x + 2u, x + 3u}, dst + v);
+            list_store4<kListAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
         }
         const uint32_t e = head + 4u * nv + id;
         if (e < P.n)
-            P.qidx[e] = e;
+            list_store1<kListAux>(lo, e, e);
         return;
     }
 
@@ -1436,7 +1319,8 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         cs[b] = a;
         ve[b] = a;
     }
-    u32x4 pk[kLineGroups], qk[kLineGroups];
+    const ListOut lout = list_out(P.qidx, P.n);
+    u32x4 pk[kG], qk[kG];
     uint32_t pt[kLineTabRegs], pend = 0;
     auto load_span = [&](uint32_t g) {
         const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
@@ -1455,7 +1339,9 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
             const uint32_t step = (kLineBlock >> P.gshift) * P.ncol * 4u;
 #pragma unroll
             for (uint32_t k = 0; k < kLineTabRegs; ++k)
-                pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, (int)(c0 * 4u + k * step), 0);
+                if (k * kLineBlock < ntab)   // (uniform)
+                    pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo,
+                                                                 (int)(c0 * 4u + k * step), 0);
             pend = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(tt * P.ncol * 4u),
                                                         (int)((c0 + ncs) * 4u), 0);
         } else {
@@ -1477,7 +1363,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
 #pragma unroll
         for (uint32_t k = 0; k < kLineTabRegs; ++k) {
             const uint32_t e = k * kLineBlock + t;
-            if (e < ntab)
+            if (k * kLineBlock < ntab && e < ntab)
                 tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k];
         }
         if (t < nb)
@@ -1555,11 +1441,15 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         // base: the slot is clamped and the hole it leaves is reported)
         auto place = [&](auto ragged) {
 #pragma unroll
-            for (uint32_t k = 0; k < kLineGroups; ++k) {
+            for (uint32_t k = 0; k < kG; ++k) {
                 const uint32_t o8 = 8u * (k * kLineBlock + t);
                 // chunks are multiples of 8 packets (clamped: groups past a short span)
                 const uint32_t cc = min(o8 >> P.cshift, ncs - 1u);
                 const uint32_t id = p0 + o8;
+                // the group's eight slot bases are read before any stage
+                // write: a read after a write to the same LDS is ordered
+                // behind it, one round trip per packet
+                uint32_t slot[8];
 #pragma unroll
                 for (uint32_t j = 0; j < 8u; ++j) {
                     const uint32_t w = (pk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu;
@@ -1572,12 +1462,15 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
                                       P.nq);
                         rk = w;
                     }
-                    if (!decltype(ragged)::value || o8 + j < len)
-                        stg[min(tab[b * rs + cc] + rk, cap)] = id + j;
+                    slot[j] = tab[__umul24(b, rs) + cc] + rk;
                 }
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j)
+                    if (!decltype(ragged)::value || o8 + j < len)
+                        stg[min(slot[j], cap)] = id + j;
             }
         };
-        if (len == P.seg)
+        if (len == line_span_max(kG))   // a whole span of the largest size: no lane is past it
             place(std::false_type{});
         else
             place(std::true_type{});
@@ -1588,15 +1481,14 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         // (e) copy-out, a quad per thread: whole lines as 16-byte non-temporal
         // stores; the bucket's last line, if the span ends inside it, is
         // carried (unless the range ends here); partial lines word by word
-        for (uint32_t v = t; v < 4u * L; v += kLineBlock) {
-            const uint32_t l = v >> 2, tag = ltag[l], mode = tag >> 30;
-            const uint32_t a0 = 16u * lgl[l] + 4u * (v & 3u);
-            const u32x4 e = reinterpret_cast<const u32x4 *>(stg)[v];
+        auto copy_quad = [&](uint32_t v, uint32_t tag, uint32_t gl, const u32x4 &e) {
+            const uint32_t mode = tag >> 30;
+            const uint32_t a0 = 16u * gl + 4u * (v & 3u);
             if (mode == 0u) {
                 const bool hole = e.x == kHole || e.y == kHole || e.z == kHole || e.w == kHole;
                 const uint32_t d = a0 - ph;
                 if (!hole && d + 4u <= P.n && d + 4u > d) {
-                    __builtin_nontemporal_store(e, reinterpret_cast<u32x4 *>(P.qidx + d));
+                    list_store4<kListAux>(lout, d, e);
                     wrote += 4u;
                 } else {
                     report_fault(P.fault, hole ? YRSS_FAULT_STAGE : YRSS_FAULT_LIST_RANGE,
@@ -1611,7 +1503,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
                         continue;
                     const uint32_t w = e[j], d = a - ph;
                     if (w != kHole && d < P.n) {
-                        P.qidx[d] = w;
+                        list_store1<kListAux>(lout, d, w);
                         ++wrote;
                     } else {
                         report_fault(P.fault, w == kHole ? YRSS_FAULT_STAGE : YRSS_FAULT_LIST_RANGE,
@@ -1619,6 +1511,23 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
                     }
                 }
             }
+        };
+        // two quads a turn, both loaded before either is stored
+        for (uint32_t v = t; v < 4u * L; v += 2u * kLineBlock) {
+            const uint32_t v2 = v + kLineBlock;
+            const bool two = v2 < 4u * L;
+            const uint32_t ta = ltag[v >> 2], ga = lgl[v >> 2];
+            const u32x4 ea = reinterpret_cast<const u32x4 *>(stg)[v];
+            uint32_t tb = 1u << 30, gb = 0u;
+            u32x4 eb = {0u, 0u, 0u, 0u};
+            if (two) {
+                tb = ltag[v2 >> 2];
+                gb = lgl[v2 >> 2];
+                eb = reinterpret_cast<const u32x4 *>(stg)[v2];
+            }
+            copy_quad(v, ta, ga, ea);
+            if (two)
+                copy_quad(v2, tb, gb, eb);
         }
         // (f) carry the unfinished last lines
         if (!last) {
@@ -2605,10 +2514,13 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     const uint64_t slots = std::max<uint32_t>(1u, kCntWords / c->nb);
     const uint64_t max_chunks = std::min<uint64_t>(kMaxChunks, waves * slots);
     const uint64_t tiles = ((uint64_t)n + kTile - 1) / kTile;
-    // the ranked scatter keeps 2 x (span chunks) prefixes per bucket (at most
-    // 64 kTab words a wave): 4-tile chunks up to 68 buckets (64 lcores and
-    // the drop bucket), 8 to 136, 16 to 272 (every bucket count)
-    const uint64_t ct_nb = c->nb <= 68u ? 4u : c->nb <= 136u ? 8u : 16u;
+    // Fewer, larger chunks mean fewer per-chunk counts for the parse kernel
+    // to flush and the scan to pass over, but a coarser deal of the batch to
+    // the parse waves: 4 tiles up to 16 buckets (8 tiles cost the parse ~7 us
+    // at 9 buckets), 8 tiles to 128 (the scan 9.8 -> 6.4 us at 65 buckets,
+    // r03 A/B; the bucket still packs beside a 9-bit rank), 16 beyond (the
+    // parse's count slots: 16 chunks a wave x nb <= kCntWords)
+    const uint64_t ct_nb = c->nb <= 16u ? 4u : c->nb <= 128u ? 8u : 16u;
     uint64_t ct = std::max<uint64_t>(c->tune.chunk_tiles ? c->tune.chunk_tiles : ct_nb,
                                      (tiles + max_chunks - 1) / max_chunks);
     uint32_t ct_shift = 0;
@@ -2628,27 +2540,21 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     return L;
 }
 
-// LDS of one scatter wave: the per-bucket arrays (aux words: four, plus the
-// placement offsets of every chunk of a span when ranked, two more when
-// self-ranked) and the stage (a piece plus up to 3 words of alignment padding
-// per bucket); wpb waves per workgroup, halved until a workgroup holds at most
-// 64 KiB.  ranked: the parse kernel's ranks place packets; it needs a span of
-// at most one piece and its offset table in the wave's share.
+// LDS of one wave of the fallback scatter (yrss_scatter): six per-bucket
+// arrays and the stage (a piece plus up to 3 words of alignment padding per
+// bucket); wpb waves per workgroup, halved until a workgroup holds at most
+// 64 KiB.
 struct ScatterLds {
     uint32_t aux, stg, wlds, wpb;
-    bool ranked;
 };
 constexpr uint32_t kScatterLdsMax = 64u * 1024u / 4u;   // words per workgroup
 
-ScatterLds scatter_lds(uint32_t nb, const Layout &lay)
+ScatterLds scatter_lds(uint32_t nb)
 {
     ScatterLds r;
-    const uint32_t nc = 1u << lay.shift;
     r.stg = (kPiece + 3u * nb + 3u) & ~3u;
-    r.ranked = lay.seg <= kPiece && nb * 2u * nc <= kTab * kWave &&
-               (4u + 2u * nc) * nb + r.stg + 4u <= kScatterLdsMax;
-    r.aux = ((r.ranked ? 4u + 2u * nc : 6u) * nb + 3u) & ~3u;
-    r.wlds = r.aux + r.stg + 4u;   // + the ranked placement's spare word
+    r.aux = (6u * nb + 3u) & ~3u;
+    r.wlds = r.aux + r.stg;
     r.wpb = (uint32_t)kScatterWaves;
     while (r.wpb > 1 && r.wpb * r.wlds > kScatterLdsMax)
         r.wpb /= 2;
@@ -2661,17 +2567,19 @@ ScatterLds scatter_lds(uint32_t nb, const Layout &lay)
 // than a span can be (batches past ~2^29 packets) or the LDS would not fit.
 struct LinePlan {
     bool ok, packed;
-    uint32_t gshift, seg, lmax, lds;
+    uint32_t groups, gshift, seg, lmax, lds;
 };
 
 LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
 {
     LinePlan p{};
     const uint32_t nb = c->nb, cshift = lay.ct_shift + 6u;
-    if (lay.chunk > kLineSpanMax || nb > (uint32_t)kLineBlock)
+    p.groups = nb > 128u ? 4u : 2u;
+    const uint32_t smax = line_span_max(p.groups);
+    if (lay.chunk > smax || nb > (uint32_t)kLineBlock)
         return p;
-    uint64_t target = c->tune.span_tiles ? (uint64_t)c->tune.span_tiles * kTile : kLineSpanMax;
-    target = std::min<uint64_t>(std::max<uint64_t>(target, lay.chunk), kLineSpanMax);
+    uint64_t target = c->tune.span_tiles ? (uint64_t)c->tune.span_tiles * kTile : smax;
+    target = std::min<uint64_t>(std::max<uint64_t>(target, lay.chunk), smax);
     p.gshift = 0;
     while (((uint64_t)lay.chunk << (p.gshift + 1)) <= target &&
            ((uint64_t)nb << (p.gshift + 1)) <= kLineTabMax)
@@ -2685,9 +2593,6 @@ LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
         return p;
     // bucket << cshift | rank fits 16 bits
     p.packed = cshift < 16u && nb <= (1u << (16u - cshift));
-#ifdef YRSS_AB_NOPACK
-    p.packed = false;
-#endif
     p.ok = true;
     return p;
 }
@@ -3441,7 +3346,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     const uint64_t pwaves = (uint64_t)grid * (kParseBlock / kWave);
     if (compact && ((uint64_t)lay.nchunk + pwaves - 1) / pwaves * c->nb > kCntWords)
         return -EINVAL;   // layout_for sizes chunks so a wave's count slots fit
-    const ScatterLds sl = scatter_lds(c->nb, lay);
+    const ScatterLds sl = scatter_lds(c->nb);
     const LinePlan lp = line_plan(c, lay);
     // the line scatter reads q (when the bucket is not packed with the rank)
     // as 16-byte vectors
@@ -3525,7 +3430,9 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         // persistent: the resident workgroups, each one contiguous range of
         // spans, never more workgroups than spans
         const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
-        void (*fn)(LineParams) = lp.packed ? yrss_scatter_lines<true> : yrss_scatter_lines<false>;
+        void (*fn)(LineParams) =
+            lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
+                            : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
         const uint32_t sgrid =
             std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
         Timed t(c, YRSS_K_SCATTER);
@@ -3549,7 +3456,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     S.ncol = lay.ncol;
     S.gshift = lay.shift;
     S.cshift = lay.ct_shift + 6u;
-    S.rank = ranked ? c->d_rank : nullptr;
     S.aux = sl.aux;
     S.stg = sl.stg;
     S.wlds = sl.wlds;
@@ -3559,7 +3465,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         const uint32_t lds = (uint32_t)(sl.wpb * sl.wlds * sizeof(uint32_t));
         const uint32_t spans = (uint32_t)(((uint64_t)n + lay.seg - 1) / lay.seg);
         uint32_t sgrid = (spans + sl.wpb - 1) / sl.wpb;
-        void (*fn)(ScatterParams) = ranked ? yrss_scatter<true> : yrss_scatter<false>;
+        void (*fn)(ScatterParams) = yrss_scatter;
         sgrid = std::min(sgrid, resident_blocks(c, (const void *)fn, sl.wpb * kWave, lds));
         Timed t(c, YRSS_K_SCATTER);
         hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(sl.wpb * kWave), lds, s, t.a,

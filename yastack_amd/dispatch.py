@@ -87,9 +87,10 @@ class SoftRss:
     def __init__(self, nb_procs: int = 3, nb_queues: int | None = None,
                  soft_dispatch: int = 1, dispatch_only_core: int = 1,
                  rss_key: bytes | None = None, device: int = 0,
-                 max_burst: int = 1 << 16):
-        self._lib = abi.load()
-        cfg = abi.default_config()
+                 max_burst: int = 1 << 16, lib_path: str | None = None):
+        self._lib = abi.load(lib_path)
+        cfg = abi.Config()
+        self._lib.yrss_config_default(ctypes.byref(cfg))
         if rss_key is not None:
             if not 4 <= len(rss_key) <= abi.RSS_KEY_LEN:
                 raise ValueError("rss_key must be 4..40 bytes")
