@@ -1,7 +1,7 @@
 #!/bin/bash
 # PMC passes (one rocprofv3 --pmc run each, counters within gfx950's per-block
 # limits) over the all-TCP bench at the given nb_procs; summarized per kernel
-# (tools/pmc_summary.py).  Usage: tools/gpu_pmc.sh TAG "3 8 64 255" [extra bench args]
+# (tools/pmc_kernels.py).  Usage: tools/gpu_pmc.sh TAG "3 8 64 255" [extra bench args]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 tag=$1
@@ -25,6 +25,6 @@ for np in $qs; do
             -- python bench.py $B > $d.log 2>&1 || { echo "pmc q$np pass $i rc=$?"; exit 1; }
     done
     echo "== q$np" >> "$out"
-    python tools/pmc_summary.py gpurun_out/pmc_${tag}_q${np}_p* >> "$out" || exit 1
+    python tools/pmc_kernels.py gpurun_out/pmc_${tag}_q${np}_p* >> "$out" || exit 1
 done
 cat "$out"

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Phase clock of the line scatter (a YRSS_PROF_LINES build): per workgroup
+and span, the 100 MHz realtime clock at each phase boundary, read by thread 0;
+prints the mean time per phase over workgroups and spans, and the spread of
+the workgroups' start and end.
+
+    tools/build_ab_lib.sh prof -DYRSS_PROF_LINES=1
+    python tools/line_prof.py --lib ab/lib/libyrss_prof.so --nb-procs 8,64
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+import torch  # noqa: E402
+
+from yastack_amd import SoftRss, abi  # noqa: E402
+
+PH = ["a tab->LDS + S1", "b layout + S2", "c slots/fill/tags", "d place", "prefetch + S4",
+      "e copy-out", "f carry"]
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lib", required=True)
+    ap.add_argument("--nb-procs", default="8,64")
+    ap.add_argument("--pkts", type=int, default=1 << 24)
+    args = ap.parse_args()
+    lib = abi.load(str(ROOT / args.lib))
+    lib.yrss_debug_line_prof.restype = ctypes.c_int
+    lib.yrss_debug_line_prof.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    n = args.pkts
+    for npr in (int(x) for x in args.nb_procs.split(",")):
+        e = SoftRss(npr, npr, 1, 1, device=0, max_burst=0, lib_path=str(ROOT / args.lib))
+        w, l = e.synth(abi.SYN_TCP4, n, 0)
+        out = e.alloc_out(n, w.device)
+        for _ in range(5):
+            e.dispatch_dev(w, l, 64, n, out=out)
+        torch.cuda.synchronize()
+        buf = np.zeros(2048 * 8 * 8, np.uint64)
+        assert lib.yrss_debug_line_prof(buf.ctypes.data, buf.nbytes) > 0
+        p = buf.reshape(2048, 8, 8).astype(np.int64)
+        used = p[:, :, 0] != 0
+        blocks = int(used[:, 0].sum())
+        spans = used.sum(axis=1)
+        d = np.diff(p, axis=2) * 10  # ns
+        m = used[:, :, None] & (p[:, :, 1:] != 0) & (p[:, :, :-1] != 0)
+        print(f"q{npr}: {blocks} workgroups, spans per workgroup {spans.min()}-{spans.max()}")
+        for k, name in enumerate(PH):
+            v = d[:, :, k][m[:, :, k]]
+            print(f"   {name:20s} mean {v.mean():8.0f} ns  p90 {np.percentile(v, 90):8.0f}")
+        first = p[:, 0, 0][used[:, 0]]
+        lastidx = spans - 1
+        ends = np.array([p[b, lastidx[b], 7] for b in range(2048) if used[b, 0]])
+        t0 = first.min()
+        print(f"   workgroup start spread {(first.max() - t0) * 10:.0f} ns, "
+              f"end {(ends.min() - t0) * 10:.0f}-{(ends.max() - t0) * 10:.0f} ns after the first start")
+        per_span = (p[:, :, 7] - p[:, :, 0])[used] * 10
+        print(f"   span total mean {per_span.mean():.0f} ns")
+        e.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1235,6 +1235,22 @@ __device__ __forceinline__ void load_groups(const uint16_t *a, uint32_t p0, uint
     }
 }
 
+#ifdef YRSS_PROF_LINES
+// measurement builds only (tools/line_prof.py): per workgroup and span, the
+// realtime clock at each phase boundary, read by thread 0
+__device__ uint64_t g_line_prof[2048 * 8 * 8];
+#define LPROF(k)                                                                       \
+    do {                                                                               \
+        if (t == 0 && blockIdx.x < 2048u && g - g0 < 8u)                              \
+            g_line_prof[(blockIdx.x * 8u + (g - g0)) * 8u + (k)] =                     \
+                __builtin_amdgcn_s_memrealtime();                                      \
+    } while (0)
+#else
+#define LPROF(k) \
+    do {         \
+    } while (0)
+#endif
+
 template <bool kPacked, uint32_t kG>
 __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P)
 {
@@ -1359,6 +1375,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
     for (uint32_t g = g0; g < g1; ++g) {
         const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
         const bool last = g + 1u == g1;
+        LPROF(0);
         // (a) the span's prefixes: tab[b][c] at chunk c, tend[b] at its end
 #pragma unroll
         for (uint32_t k = 0; k < kLineTabRegs; ++k) {
@@ -1369,6 +1386,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         if (t < nb)
             tend[t] = pend;
         __syncthreads();
+        LPROF(1);
         // (b) per bucket: the valid positions [cs, ve) = the carried words and
         // the span's packets; its stage lines (exclusive scan), stage offset
         // and the prefix rows' bias
@@ -1406,6 +1424,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
             }
         }
         __syncthreads();
+        LPROF(2);
         const uint32_t L = __builtin_amdgcn_readfirstlane(misc[2]);
         // (c) prefix rows -> stage slots; stage pre-filled with the hole mark;
         // each stage line tagged with its bucket, list line and copy mode
@@ -1431,6 +1450,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
             lgl[l] = gl;
         }
         __syncthreads();
+        LPROF(3);
         // (d) the carried words, then every packet at its slot
         for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
             const uint32_t b = e >> 4, j = e & 15u;
@@ -1475,9 +1495,11 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         else
             place(std::true_type{});
         // the next span's streams and prefixes are in flight during the copy-out
+        LPROF(4);
         if (!last)
             load_span(g + 1u);
         __syncthreads();
+        LPROF(5);
         // (e) copy-out, a quad per thread: whole lines as 16-byte non-temporal
         // stores; the bucket's last line, if the span ends inside it, is
         // carried (unless the range ends here); partial lines word by word
@@ -1529,6 +1551,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
             if (two)
                 copy_quad(v2, tb, gb, eb);
         }
+        LPROF(6);
         // (f) carry the unfinished last lines
         if (!last) {
             for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
@@ -1538,6 +1561,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
                     cb[e] = stg[min(so[b] + nv + j, cap)];
             }
         }
+        LPROF(7);
     }
     // every packet of the range left exactly once
     wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
@@ -3478,6 +3502,18 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
 }  // namespace
 
 extern "C" {
+
+#ifdef YRSS_PROF_LINES
+// measurement builds only: the line scatter's phase clock (tools/line_prof.py)
+int yrss_debug_line_prof(void *out, size_t bytes)
+{
+    const size_t n = bytes < sizeof(g_line_prof) ? bytes : sizeof(g_line_prof);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_line_prof), n, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess
+               ? (int)n
+               : -EIO;
+}
+#endif
 
 int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
                       const uint16_t *d_len, uint32_t n, int16_t *d_q, uint32_t *d_hash,
