@@ -39,8 +39,9 @@ def main() -> int:
     ap.add_argument("--batches", type=int, default=4)
     ap.add_argument("--profile", default="tcp4", choices=sorted(PROFILES))
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--tune", default="", help="k=v[,k=v] for every build, or per build "
-                    "as lib@k=v in --libs")
+    ap.add_argument("--tune", default="", help="k=v[;k=v] for every build, or per build "
+                    "as lib@k=v in --libs (yrss_set_tuning fields, and pipe=1 for "
+                    "pipelined batches)")
     args = ap.parse_args()
     n, stride = args.pkts, 64
     specs = []
@@ -64,8 +65,10 @@ def main() -> int:
                 spacer = torch.empty(rng.randrange(0, 64) << 21, dtype=torch.uint8,
                                      device="cuda")
                 e = SoftRss(npr, npr, 1, 1, device=0, max_burst=0, lib_path=path)
-                if tune:
-                    e.set_tuning(**tune)
+                tn = dict(tune)
+                pipe = bool(tn.pop("pipe", 0))
+                if tn:
+                    e.set_tuning(**tn)
                 wins = [e.synth(PROFILES[args.profile], n, k * n, stride=stride)
                         for k in range(args.batches)]
                 outs = [e.alloc_out(n, wins[0][0].device) for _ in range(args.batches)]
@@ -75,7 +78,8 @@ def main() -> int:
                     for _ in range(steps):
                         k = it[0] % args.batches
                         it[0] += 1
-                        e.dispatch_dev(wins[k][0], wins[k][1], stride, n, out=outs[k])
+                        e.dispatch_dev(wins[k][0], wins[k][1], stride, n, out=outs[k],
+                                       pipeline=pipe)
 
                 run(4)
                 torch.cuda.synchronize()

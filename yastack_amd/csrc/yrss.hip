@@ -2386,14 +2386,27 @@ struct yrss_ctx {
         uint32_t block, lds, blocks;
     };
     std::vector<Occ> occ;           // resident_blocks cache
-    uint16_t *d_rank = nullptr;     // ranked scatter workspace (n x u16), grown on demand
-    size_t rank_cap = 0;
-    unsigned long long *d_scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
+    // The lists' workspace: per-chunk counts and prefixes, totals, scan
+    // status, ranks.  Two sets: a pipelined batch (yrss_dispatch_dev_pipelined)
+    // builds its lists on the lists stream with one set while the next
+    // batch's parse kernel fills the other.
+    struct ListWs {
+        uint32_t *seg_cnt = nullptr;
+        uint32_t *seg_off = nullptr;
+        uint32_t *totals = nullptr;
+        unsigned long long *scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
+        uint32_t scan_epoch = 0;
+        uint16_t *rank = nullptr;    // n x u16, grown on demand
+        size_t rank_cap = 0;
+        hipEvent_t parsed = nullptr;   // pipeline: the batch's parse kernel is done
+        hipEvent_t done = nullptr;     // pipeline: its lists are done
+        bool pending = false;          // lists queued on lstream, not yet joined
+    };
+    ListWs ws[2];
+    uint32_t pipe_next = 0;
+    hipStream_t lstream = nullptr;     // pipeline: scan + scatter, on its own CUs
+    uint32_t lstream_cus = 0;
     uint32_t *d_fault_rec = nullptr;    // host-coherent fault record {code, kernel, where, value}
-    uint32_t scan_epoch = 0;
-    uint32_t *d_seg_cnt = nullptr;
-    uint32_t *d_seg_off = nullptr;
-    uint32_t *d_totals = nullptr;
     // host-burst staging (pinned) and its device mirror
     hipStream_t stream = nullptr;
     uint32_t burst_cap = 0;
@@ -2883,7 +2896,75 @@ bool take_fault(yrss_ctx *c, yrss_fault *out = nullptr)
     return true;
 }
 
-int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream);
+int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
+                      bool pipe = false);
+
+// One set of the lists' workspace (the count matrix zeroed: the parse kernel
+// writes only the columns of the launch)
+hipError_t list_ws_alloc(yrss_ctx *c, yrss_ctx::ListWs &w)
+{
+    const size_t cnt = (size_t)kMaxChunks * c->nb * sizeof(uint32_t);
+    const size_t st = (size_t)c->nb * (kMaxChunks / kScanTile) * sizeof(unsigned long long);
+    hipError_t e;
+    if ((e = hipMalloc((void **)&w.seg_cnt, cnt)) != hipSuccess ||
+        (e = hipMalloc((void **)&w.seg_off, cnt)) != hipSuccess ||
+        (e = hipMalloc((void **)&w.totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc((void **)&w.scan_status, st)) != hipSuccess ||
+        (e = hipMemset(w.scan_status, 0, st)) != hipSuccess ||
+        (e = hipMemset(w.seg_cnt, 0, cnt)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&w.parsed, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming)) != hipSuccess)
+        return e;
+    return hipSuccess;
+}
+
+void list_ws_free(yrss_ctx::ListWs &w)
+{
+    (void)hipFree(w.seg_cnt);
+    (void)hipFree(w.seg_off);
+    (void)hipFree(w.totals);
+    (void)hipFree(w.scan_status);
+    (void)hipFree(w.rank);
+    if (w.parsed)
+        (void)hipEventDestroy(w.parsed);
+    if (w.done)
+        (void)hipEventDestroy(w.done);
+    w = yrss_ctx::ListWs{};
+}
+
+// Order stream s after every pipelined batch's lists not yet joined.
+int join_lists(yrss_ctx *c, hipStream_t s)
+{
+    for (auto &w : c->ws)
+        if (w.pending) {
+            YRSS_HIP(hipStreamWaitEvent(s, w.done, 0));
+            w.pending = false;
+        }
+    return 0;
+}
+
+// The lists stream of pipelined batches: its own CUs (every eighth CU by
+// default, yrss_tuning.list_cus), so its workgroups never sit on the CUs the
+// next batch's parse kernel is dealt to.
+int lists_stream(yrss_ctx *c)
+{
+    const uint32_t want = c->tune.list_cus ? c->tune.list_cus : (uint32_t)c->cus / 8u;
+    if (c->lstream && c->lstream_cus == want)
+        return 0;
+    if (c->lstream) {
+        YRSS_HIP(hipStreamSynchronize(c->lstream));
+        (void)hipStreamDestroy(c->lstream);
+        c->lstream = nullptr;
+    }
+    std::vector<uint32_t> mask(((uint32_t)c->cus + 31u) / 32u, 0u);
+    const uint32_t step = std::max(1u, (uint32_t)c->cus / want);
+    uint32_t got = 0;
+    for (uint32_t i = step - 1u; i < (uint32_t)c->cus && got < want; i += step, ++got)
+        mask[i / 32u] |= 1u << (i % 32u);
+    YRSS_HIP(hipExtStreamCreateWithCUMask(&c->lstream, (uint32_t)mask.size() * 32u, mask.data()));
+    c->lstream_cus = got;
+    return 0;
+}
 
 bool small_ok(const yrss_ctx *c, uint32_t n)
 {
@@ -3186,14 +3267,9 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
 
     const size_t ws = (size_t)kMaxChunks * c->nb * sizeof(uint32_t);
     hipError_t e;
-    if ((e = hipMalloc((void **)&c->d_seg_cnt, ws)) != hipSuccess ||
-        (e = hipMalloc((void **)&c->d_seg_off, ws)) != hipSuccess ||
-        (e = hipMalloc((void **)&c->d_totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMalloc((void **)&c->d_scan_status, (size_t)c->nb * (kMaxChunks / kScanTile) *
-                                                       sizeof(unsigned long long))) != hipSuccess ||
+    (void)ws;
+    if ((e = list_ws_alloc(c, c->ws[0])) != hipSuccess ||
         (e = hipHostMalloc((void **)&c->d_fault_rec, 64, hipHostMallocCoherent)) != hipSuccess ||
-        (e = hipMemset(c->d_scan_status, 0, (size_t)c->nb * (kMaxChunks / kScanTile) *
-                                                sizeof(unsigned long long))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_kni, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_fault, sizeof(uint32_t))) != hipSuccess ||
         (e = hipHostMalloc((void **)&c->h_fault, sizeof(uint32_t), hipHostMallocCoherent)) !=
@@ -3202,7 +3278,6 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
         (e = hipHostMalloc((void **)&c->h_done, 64, hipHostMallocCoherent)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void **)&c->dh_done, c->h_done, 0)) != hipSuccess ||
         (e = hipMemset(c->d_kni, 0, sizeof(c->kni_bm))) != hipSuccess ||
-        (e = hipMemset(c->d_seg_cnt, 0, ws)) != hipSuccess ||
         (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming)) != hipSuccess) {
         yrss_fini(c);
@@ -3251,12 +3326,11 @@ void yrss_fini(yrss_ctx *c)
     for (auto e : c->ev_free)
         (void)hipEventDestroy(e);
     free_burst(c);
-    (void)hipFree(c->d_seg_cnt);
-    (void)hipFree(c->d_seg_off);
-    (void)hipFree(c->d_scan_status);
-    (void)hipFree(c->d_rank);
+    for (auto &w : c->ws)
+        list_ws_free(w);
+    if (c->lstream)
+        (void)hipStreamDestroy(c->lstream);
     (void)hipHostFree(c->d_fault_rec);
-    (void)hipFree(c->d_totals);
     (void)hipFree(c->d_kni);
     (void)hipFree(c->d_fault);
     (void)hipHostFree(c->h_fault);
@@ -3308,11 +3382,37 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     return dispatch_dev_impl(c, b, stream);
 }
 
+int yrss_dispatch_dev_pipelined(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
+{
+    if (!c || !b)
+        return -EINVAL;
+    if (c->pend.active)
+        return -EBUSY;
+    return dispatch_dev_impl(c, b, stream, true);
+}
+
+int yrss_dispatch_join(yrss_ctx *c, void *stream)
+{
+    if (!c)
+        return -EINVAL;
+    return join_lists(c, (hipStream_t)stream);
+}
+
 }  // extern "C"
 
 namespace {
 
-int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
+// A pipelined batch's lists are queued: mark the set pending until a join.
+int finish_lists(yrss_ctx *c, yrss_ctx::ListWs &W, bool pipe)
+{
+    if (pipe) {
+        YRSS_HIP(hipEventRecord(W.done, c->lstream));
+        W.pending = true;
+    }
+    return 0;
+}
+
+int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream, bool pipe)
 {
     const uint32_t n = b->n, win_stride = b->win_stride;
     if (win_stride < YRSS_WIN_MIN || (win_stride & 15u) || n > YRSS_MAX_BATCH)
@@ -3327,6 +3427,10 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     if (compact && !b->qstart)
         return -EINVAL;
     hipStream_t s = (hipStream_t)stream;
+    // A batch that is not pipelined uses workspace set 0 on `s` alone: every
+    // pipelined batch's lists come first.
+    if (!pipe && join_lists(c, s) != 0)
+        return -EIO;
     if (n == 0) {
         if (compact)
             YRSS_HIP(hipMemsetAsync(b->qstart, 0, (c->nb + 1) * sizeof(uint32_t), s));
@@ -3344,6 +3448,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     if (c->last_stream_valid && c->last_stream != s) {
         YRSS_HIP(hipEventRecord(c->switch_ev, c->last_stream));
         YRSS_HIP(hipStreamWaitEvent(s, c->switch_ev, 0));
+        if (join_lists(c, s) != 0)
+            return -EIO;
     }
     c->last_stream = s;
     c->last_stream_valid = true;
@@ -3365,7 +3471,35 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         S.qstart = compact ? b->qstart : nullptr;
         return small_launch(c, S, filter, false, s);
     }
-    const uint32_t grid = grid_for(c, n);
+    // pipelined: workspace sets alternate (the set's previous lists must be
+    // done before this parse kernel overwrites it), and the parse kernel
+    // leaves the lists stream's CUs free
+    uint32_t k = 0;
+    if (pipe && compact) {
+        if (lists_stream(c) != 0)
+            return -EIO;
+        k = c->pipe_next;
+        c->pipe_next ^= 1u;
+        auto &w = c->ws[k];
+        if (!w.seg_cnt) {
+            const hipError_t e = list_ws_alloc(c, w);
+            if (e != hipSuccess) {
+                list_ws_free(w);
+                return hip_fail("pipeline workspace", e);
+            }
+            YRSS_HIP(hipDeviceSynchronize());   // the memsets ran on the null stream
+        }
+        if (w.pending) {
+            YRSS_HIP(hipStreamWaitEvent(s, w.done, 0));
+            w.pending = false;
+        }
+    } else {
+        pipe = false;
+    }
+    yrss_ctx::ListWs &W = c->ws[k];
+    uint32_t grid = grid_for(c, n);
+    if (pipe && !c->tune.parse_blocks)
+        grid = std::min(grid, (uint32_t)c->cus - c->lstream_cus);
     const Layout lay = layout_for(c, n, grid);
     const uint64_t pwaves = (uint64_t)grid * (kParseBlock / kWave);
     if (compact && ((uint64_t)lay.nchunk + pwaves - 1) / pwaves * c->nb > kCntWords)
@@ -3375,25 +3509,28 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     // the line scatter reads q (when the bucket is not packed with the rank)
     // as 16-byte vectors
     const bool ranked = compact && lp.ok && (lp.packed || ((uintptr_t)b->q & 15u) == 0);
-    if (ranked && c->rank_cap < n) {
+    if (ranked && W.rank_cap < n) {
         // the ranks' workspace grows to the largest batch seen; the old one
-        // may still be read by a scatter queued on this stream
-        if (c->d_rank) {
+        // may still be read by a scatter queued on this stream (or, for a
+        // pipelined set, on the lists stream)
+        if (W.rank) {
             YRSS_HIP(hipStreamSynchronize(s));
-            (void)hipFree(c->d_rank);
-            c->d_rank = nullptr;
-            c->rank_cap = 0;
+            if (c->lstream)
+                YRSS_HIP(hipStreamSynchronize(c->lstream));
+            (void)hipFree(W.rank);
+            W.rank = nullptr;
+            W.rank_cap = 0;
         }
-        YRSS_HIP(hipMalloc((void **)&c->d_rank, (size_t)n * sizeof(uint16_t)));
-        c->rank_cap = n;
+        YRSS_HIP(hipMalloc((void **)&W.rank, (size_t)n * sizeof(uint16_t)));
+        W.rank_cap = n;
     }
     ParseParams P = c->proto;
     P.win = b->win;
     P.len = b->len;
     P.q = b->q;
     P.hash = b->hash;
-    P.seg_cnt = compact ? c->d_seg_cnt : nullptr;
-    P.rank = ranked ? c->d_rank : nullptr;
+    P.seg_cnt = compact ? W.seg_cnt : nullptr;
+    P.rank = ranked ? W.rank : nullptr;
     P.fault = c->d_fault_rec;
     P.n = n;
     P.stride = win_stride;
@@ -3414,20 +3551,26 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     YRSS_HIP(hipGetLastError());
     if (!compact)
         return 0;
+    if (pipe) {
+        // the lists of this batch: on the lists stream, after its parse
+        YRSS_HIP(hipEventRecord(W.parsed, s));
+        YRSS_HIP(hipStreamWaitEvent(c->lstream, W.parsed, 0));
+        s = c->lstream;
+    }
     {
         Timed t(c, YRSS_K_SCAN);
         ScanParams SP;
-        SP.cnt = c->d_seg_cnt;
-        SP.off = c->d_seg_off;
-        SP.totals = c->d_totals;
-        SP.status = c->d_scan_status;
+        SP.cnt = W.seg_cnt;
+        SP.off = W.seg_off;
+        SP.totals = W.totals;
+        SP.status = W.scan_status;
         SP.fault = c->d_fault_rec;
         SP.nchunk = lay.nchunk;
         SP.ncol = lay.ncol;
         SP.tiles = lay.ncol / kScanTile;
-        if ((++c->scan_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
-            ++c->scan_epoch;
-        SP.epoch = c->scan_epoch;
+        if ((++W.scan_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
+            ++W.scan_epoch;
+        SP.epoch = W.scan_epoch;
         hipExtLaunchKernelGGL(yrss_seg_scan, dim3(c->nb * SP.tiles), dim3(kScanBlock), 0, s,
                               t.a, t.b, 0, SP);
     }
@@ -3435,9 +3578,9 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     if (ranked) {
         LineParams S;
         S.q = b->q;
-        S.rank = c->d_rank;
-        S.seg_off = c->d_seg_off;
-        S.totals = c->d_totals;
+        S.rank = W.rank;
+        S.seg_off = W.seg_off;
+        S.totals = W.totals;
         S.qidx = b->qidx;
         S.qstart = b->qstart;
         S.fault = c->d_fault_rec;
@@ -3457,18 +3600,20 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         void (*fn)(LineParams) =
             lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
                             : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
-        const uint32_t sgrid =
-            std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
+        uint32_t sgrid = resident_blocks(c, (const void *)fn, kLineBlock, lp.lds);
+        if (pipe)   // resident on the lists stream's CUs only
+            sgrid = std::max(1u, sgrid / (uint32_t)c->cus * c->lstream_cus);
+        sgrid = std::min(spans, sgrid);
         Timed t(c, YRSS_K_SCATTER);
         hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(kLineBlock), lp.lds, s, t.a,
                               t.b, 0, S);
         YRSS_HIP(hipGetLastError());
-        return 0;
+        return finish_lists(c, W, pipe);
     }
     ScatterParams S;
     S.q = b->q;
-    S.seg_off = c->d_seg_off;
-    S.totals = c->d_totals;
+    S.seg_off = W.seg_off;
+    S.totals = W.totals;
     S.qidx = b->qidx;
     S.qstart = b->qstart;
     S.fault = c->d_fault_rec;
@@ -3496,7 +3641,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
                               t.b, 0, S);
     }
     YRSS_HIP(hipGetLastError());
-    return 0;
+    return finish_lists(c, W, pipe);
 }
 
 }  // namespace
@@ -4444,7 +4589,8 @@ int yrss_set_tuning(yrss_ctx *c, const struct yrss_tuning *t)
     const bool pow2 = (t->chunk_tiles & (t->chunk_tiles - 1u)) == 0 &&
                       (t->span_tiles & (t->span_tiles - 1u)) == 0;
     if (!pow2 || t->chunk_tiles > 4096u || t->span_tiles > 65536u || t->parse_blocks > 65536u ||
-        t->one_launch > 2u || t->scatter_xcd < -1 || t->scatter_xcd > 1)
+        t->one_launch > 2u || t->scatter_xcd < -1 || t->scatter_xcd > 1 ||
+        t->list_cus > (uint32_t)c->cus / 2u)
         return -EINVAL;
     if (c->pend.active)
         return -EBUSY;
