@@ -77,10 +77,6 @@ def parse_args(argv=None):
                          "(0: diagnosis only, roofline.achieved is then null)")
     ap.add_argument("--pmc", default=str(ROOT / "profiles" / "pmc_parse_hash.json"),
                     help="rocprofv3 PMC summary used for roofline.traffic")
-    ap.add_argument("--pipeline", type=int, default=0,
-                    help="1: pipelined batches (yrss_dispatch_dev_pipelined): each batch's "
-                         "lists are built on the context's lists stream while the next "
-                         "batch is parsed; the timed region still ends with a device sync")
     ap.add_argument("--tune", default="",
                     help="layout overrides for measurements, k=v[,k=v] (yrss_set_tuning "
                          "fields: chunk_tiles, span_tiles, parse_blocks, scatter_xcd)")
@@ -561,8 +557,7 @@ def main(argv=None):
     def step():
         w_k, l_k, o_k = batches[it[0] % nbat]
         it[0] += 1
-        eng.dispatch_dev(w_k, l_k, args.stride, n, out=o_k, compact=not args.no_compact,
-                         pipeline=bool(args.pipeline))
+        eng.dispatch_dev(w_k, l_k, args.stride, n, out=o_k, compact=not args.no_compact)
 
     probe_s = probe_traffic(batches, n, args.stride, max(args.steps, 10))
     probe_rd_s = probe_traffic(batches, n, args.stride, max(args.steps, 10), mode=1)
@@ -678,7 +673,6 @@ def main(argv=None):
                 "dispatch_only_core": args.dispatch_only_core,
                 "per_queue_lists": not args.no_compact,
                 "kni_filter": args.filter,
-                "pipelined_lists": bool(args.pipeline),
                 "parallelism": f"shard{world}",
                 "devices": devices,
             },

@@ -192,18 +192,6 @@ struct yrss_dev_batch {
 };
 int yrss_dispatch_dev_ex(yrss_ctx *ctx, const struct yrss_dev_batch *b, void *stream);
 
-/* Pipelined device batches.  As yrss_dispatch_dev_ex, except that the batch's
- * per-queue lists (qidx / qstart: the scan and the scatter) are built on the
- * context's lists stream, on CUs of their own, while `stream` goes on to the
- * next batch's parse kernel.  q, hash and filter are ready in `stream` order
- * as usual; qidx / qstart are ready once yrss_dispatch_join has ordered
- * `stream` after them (or after a device-wide synchronisation).  Two batches'
- * lists may be in flight; a third waits for the first.  Results are identical
- * to yrss_dispatch_dev_ex.  A non-pipelined call, a host burst or a worker on
- * the context joins first. */
-int yrss_dispatch_dev_pipelined(yrss_ctx *ctx, const struct yrss_dev_batch *b, void *stream);
-/* Order `stream` after the lists of every pipelined batch queued so far. */
-int yrss_dispatch_join(yrss_ctx *ctx, void *stream);
 
 /* ---- host-resident dispatch (the drop-in burst hook) ------------------------ */
 
@@ -566,13 +554,10 @@ struct yrss_tuning {
                                 wave's count slots run out)                          */
     uint32_t span_tiles;     /* line-scatter span in tiles, power of two (default 128
                                 up to 128 buckets, 256 beyond)                       */
-    uint32_t parse_blocks;   /* parse grid (default one workgroup per CU; pipelined
-                                batches leave the lists' CUs out)                    */
+    uint32_t parse_blocks;   /* parse grid (default one workgroup per CU)            */
     uint32_t one_launch;     /* batches <= 4096 packets in one launch: 0 host bursts
                                 and device batches, 1 host bursts only, 2 never      */
     int32_t  scatter_xcd;    /* XCD-contiguous scatter ranges: -1 default (on), 0, 1 */
-    uint32_t list_cus;       /* pipelined batches: CUs of the lists stream (default
-                                CUs / 8)                                             */
 };
 int yrss_set_tuning(yrss_ctx *ctx, const struct yrss_tuning *t);
 

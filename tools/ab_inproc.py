@@ -40,8 +40,8 @@ def main() -> int:
     ap.add_argument("--profile", default="tcp4", choices=sorted(PROFILES))
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--tune", default="", help="k=v[;k=v] for every build, or per build "
-                    "as lib@k=v in --libs (yrss_set_tuning fields, and pipe=1 for "
-                    "pipelined batches)")
+                    "as lib@k=v in --libs (yrss_set_tuning fields; side=1 runs the "
+                    "batches on a non-default stream)")
     args = ap.parse_args()
     n, stride = args.pkts, 64
     specs = []
@@ -66,7 +66,8 @@ def main() -> int:
                                      device="cuda")
                 e = SoftRss(npr, npr, 1, 1, device=0, max_burst=0, lib_path=path)
                 tn = dict(tune)
-                pipe = bool(tn.pop("pipe", 0))
+                # side=1: the caller's work on a non-default (non-blocking) stream
+                st = torch.cuda.Stream() if tn.pop("side", 0) else None
                 if tn:
                     e.set_tuning(**tn)
                 wins = [e.synth(PROFILES[args.profile], n, k * n, stride=stride)
@@ -79,7 +80,7 @@ def main() -> int:
                         k = it[0] % args.batches
                         it[0] += 1
                         e.dispatch_dev(wins[k][0], wins[k][1], stride, n, out=outs[k],
-                                       pipeline=pipe)
+                                       stream=st)
 
                 run(4)
                 torch.cuda.synchronize()

@@ -148,7 +148,6 @@ class Tuning(ctypes.Structure):
         ("parse_blocks", ctypes.c_uint32),
         ("one_launch", ctypes.c_uint32),
         ("scatter_xcd", ctypes.c_int32),
-        ("list_cus", ctypes.c_uint32),
     ]
 
 
@@ -189,8 +188,6 @@ _PROTOS = {
                                           ctypes.POINTER(ctypes.c_uint64)]),
     "yrss_worker_submit_frames": (ctypes.c_int, [_vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp,
                                                  ctypes.POINTER(ctypes.c_uint64)]),
-    "yrss_dispatch_dev_pipelined": (ctypes.c_int, [_vp, ctypes.POINTER(DevBatch), _vp]),
-    "yrss_dispatch_join": (ctypes.c_int, [_vp, _vp]),
     "yrss_worker_submit_windows": (ctypes.c_int, [_vp, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp,
                                                   ctypes.POINTER(ctypes.c_uint64)]),
     "yrss_worker_poll": (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_int]),

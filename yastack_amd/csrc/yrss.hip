@@ -1252,7 +1252,7 @@ __device__ uint64_t g_line_prof[2048 * 8 * 8];
 #endif
 
 template <bool kPacked, uint32_t kG>
-__global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P)
+__global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lines(LineParams P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
     const uint32_t nb = P.nb, t = threadIdx.x, lane = lane_id();
@@ -1286,6 +1286,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
             if (blockIdx.x == 0)
                 P.qstart[nb] = carry;
             misc[0] = nzb;
+            misc[1] = 0u;
             misc[3] = 0u;
         }
     }
@@ -1371,7 +1372,10 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         }
     };
     load_span(g0);
-    uint32_t wrote = 0;
+    // words written and their sum: a range is complete iff it wrote each of
+    // its packets once, so the sum must be that of its packet indices (two
+    // packets on one slot leave another slot with an earlier span's index)
+    uint32_t wrote = 0, wsum = 0;
     for (uint32_t g = g0; g < g1; ++g) {
         const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
         const bool last = g + 1u == g1;
@@ -1426,13 +1430,10 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         __syncthreads();
         LPROF(2);
         const uint32_t L = __builtin_amdgcn_readfirstlane(misc[2]);
-        // (c) prefix rows -> stage slots; stage pre-filled with the hole mark;
-        // each stage line tagged with its bucket, list line and copy mode
-        // (0 whole, 1 carried, 2 word by word)
+        // (c) prefix rows -> stage slots; each stage line tagged with its
+        // bucket, list line and copy mode (0 whole, 1 carried, 2 word by word)
         for (uint32_t e = t; e < ntab; e += kLineBlock)
             tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] += rb[e >> P.gshift];
-        for (uint32_t v = t; v < 4u * L; v += kLineBlock)
-            reinterpret_cast<u32x4 *>(stg)[v] = u32x4{kHole, kHole, kHole, kHole};
         for (uint32_t l = t; l < L; l += kLineBlock) {
             uint32_t lo = 0, hi = nb;   // lsl[lo] <= l < lsl[hi]
             while (hi - lo > 1u) {
@@ -1460,16 +1461,18 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
         // (a packed bucket past nb reads some other LDS word as its slot
         // base: the slot is clamped and the hole it leaves is reported)
         auto place = [&](auto ragged) {
+            // every slot base of the thread's packets is read before any
+            // stage write: a read after a write to the same LDS is ordered
+            // behind it, one round trip each
+            // (two groups at a time: registers)
 #pragma unroll
-            for (uint32_t k = 0; k < kG; ++k) {
+            for (uint32_t k0 = 0; k0 < kG; k0 += 2u) {
+            uint32_t slot[2][8];
+#pragma unroll
+            for (uint32_t k = k0; k < k0 + 2u; ++k) {
                 const uint32_t o8 = 8u * (k * kLineBlock + t);
                 // chunks are multiples of 8 packets (clamped: groups past a short span)
                 const uint32_t cc = min(o8 >> P.cshift, ncs - 1u);
-                const uint32_t id = p0 + o8;
-                // the group's eight slot bases are read before any stage
-                // write: a read after a write to the same LDS is ordered
-                // behind it, one round trip per packet
-                uint32_t slot[8];
 #pragma unroll
                 for (uint32_t j = 0; j < 8u; ++j) {
                     const uint32_t w = (pk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu;
@@ -1482,12 +1485,18 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
                                       P.nq);
                         rk = w;
                     }
-                    slot[j] = tab[__umul24(b, rs) + cc] + rk;
+                    slot[k - k0][j] = tab[__umul24(b, rs) + cc] + rk;
                 }
+            }
+#pragma unroll
+            for (uint32_t k = k0; k < k0 + 2u; ++k) {
+                const uint32_t o8 = 8u * (k * kLineBlock + t);
+                const uint32_t id = p0 + o8;
 #pragma unroll
                 for (uint32_t j = 0; j < 8u; ++j)
                     if (!decltype(ragged)::value || o8 + j < len)
-                        stg[min(slot[j], cap)] = id + j;
+                        stg[min(slot[k - k0][j], cap)] = id + j;
+            }
             }
         };
         if (len == line_span_max(kG))   // a whole span of the largest size: no lane is past it
@@ -1507,14 +1516,13 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
             const uint32_t mode = tag >> 30;
             const uint32_t a0 = 16u * gl + 4u * (v & 3u);
             if (mode == 0u) {
-                const bool hole = e.x == kHole || e.y == kHole || e.z == kHole || e.w == kHole;
                 const uint32_t d = a0 - ph;
-                if (!hole && d + 4u <= P.n && d + 4u > d) {
+                if (d + 4u <= P.n && d + 4u > d) {
                     list_store4<kListAux>(lout, d, e);
                     wrote += 4u;
+                    wsum += e.x + e.y + e.z + e.w;
                 } else {
-                    report_fault(P.fault, hole ? YRSS_FAULT_STAGE : YRSS_FAULT_LIST_RANGE,
-                                 YRSS_K_SCATTER, g, d);
+                    report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
                 }
             } else if (mode == 2u) {
                 const uint32_t b = tag & 0xffffu, v0 = cs[b], e1 = ve[b];
@@ -1524,32 +1532,37 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
                     if (a < v0 || a >= e1)
                         continue;
                     const uint32_t w = e[j], d = a - ph;
-                    if (w != kHole && d < P.n) {
+                    if (d < P.n) {
                         list_store1<kListAux>(lout, d, w);
                         ++wrote;
+                        wsum += w;
                     } else {
-                        report_fault(P.fault, w == kHole ? YRSS_FAULT_STAGE : YRSS_FAULT_LIST_RANGE,
-                                     YRSS_K_SCATTER, g, d);
+                        report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
                     }
                 }
             }
         };
-        // two quads a turn, both loaded before either is stored
-        for (uint32_t v = t; v < 4u * L; v += 2u * kLineBlock) {
-            const uint32_t v2 = v + kLineBlock;
-            const bool two = v2 < 4u * L;
-            const uint32_t ta = ltag[v >> 2], ga = lgl[v >> 2];
-            const u32x4 ea = reinterpret_cast<const u32x4 *>(stg)[v];
-            uint32_t tb = 1u << 30, gb = 0u;
-            u32x4 eb = {0u, 0u, 0u, 0u};
-            if (two) {
-                tb = ltag[v2 >> 2];
-                gb = lgl[v2 >> 2];
-                eb = reinterpret_cast<const u32x4 *>(stg)[v2];
+        // kCopyQ quads a turn, all loaded before any is stored (an
+        // 8192-packet span's lines fit one turn up to ~128 buckets)
+        constexpr uint32_t kCopyQ = 5u;
+        for (uint32_t v0 = t; v0 < 4u * L; v0 += kCopyQ * kLineBlock) {
+            uint32_t tg[kCopyQ], gl[kCopyQ];
+            u32x4 eq[kCopyQ];
+#pragma unroll
+            for (uint32_t i = 0; i < kCopyQ; ++i) {
+                const uint32_t v = v0 + i * kLineBlock;
+                tg[i] = 1u << 30;   // mode 1: nothing to store
+                gl[i] = 0u;
+                eq[i] = u32x4{0u, 0u, 0u, 0u};
+                if (v < 4u * L) {
+                    tg[i] = ltag[v >> 2];
+                    gl[i] = lgl[v >> 2];
+                    eq[i] = reinterpret_cast<const u32x4 *>(stg)[v];
+                }
             }
-            copy_quad(v, ta, ga, ea);
-            if (two)
-                copy_quad(v2, tb, gb, eb);
+#pragma unroll
+            for (uint32_t i = 0; i < kCopyQ; ++i)
+                copy_quad(v0 + i * kLineBlock, tg[i], gl[i], eq[i]);
         }
         LPROF(6);
         // (f) carry the unfinished last lines
@@ -1565,13 +1578,20 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_lines(LineParams P
     }
     // every packet of the range left exactly once
     wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
-    if (lane == 0)
+    wsum = __shfl(wave_incl_scan(wsum, lane), kWave - 1, kWave);
+    if (lane == 0) {
         atomicAdd(&misc[3], wrote);
+        atomicAdd(&misc[1], wsum);
+    }
     __syncthreads();
     if (t == 0) {
-        const uint32_t want = span_end(g1 - 1u) - g0 * P.seg;
+        const uint64_t a = (uint64_t)g0 * P.seg, e = span_end(g1 - 1u);
+        const uint32_t want = (uint32_t)(e - a);
+        const uint32_t want_sum = (uint32_t)((e - a) * (a + e - 1u) / 2u);
         if (misc[3] != want)
             report_fault(P.fault, YRSS_FAULT_COUNT_MISMATCH, YRSS_K_SCATTER, g0, misc[3]);
+        else if (misc[1] != want_sum)
+            report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g0, misc[1]);
     }
 }
 
@@ -2387,9 +2407,7 @@ struct yrss_ctx {
     };
     std::vector<Occ> occ;           // resident_blocks cache
     // The lists' workspace: per-chunk counts and prefixes, totals, scan
-    // status, ranks.  Two sets: a pipelined batch (yrss_dispatch_dev_pipelined)
-    // builds its lists on the lists stream with one set while the next
-    // batch's parse kernel fills the other.
+    // status, ranks.
     struct ListWs {
         uint32_t *seg_cnt = nullptr;
         uint32_t *seg_off = nullptr;
@@ -2398,14 +2416,8 @@ struct yrss_ctx {
         uint32_t scan_epoch = 0;
         uint16_t *rank = nullptr;    // n x u16, grown on demand
         size_t rank_cap = 0;
-        hipEvent_t parsed = nullptr;   // pipeline: the batch's parse kernel is done
-        hipEvent_t done = nullptr;     // pipeline: its lists are done
-        bool pending = false;          // lists queued on lstream, not yet joined
     };
-    ListWs ws[2];
-    uint32_t pipe_next = 0;
-    hipStream_t lstream = nullptr;     // pipeline: scan + scatter, on its own CUs
-    uint32_t lstream_cus = 0;
+    ListWs ws;
     uint32_t *d_fault_rec = nullptr;    // host-coherent fault record {code, kernel, where, value}
     // host-burst staging (pinned) and its device mirror
     hipStream_t stream = nullptr;
@@ -2896,11 +2908,10 @@ bool take_fault(yrss_ctx *c, yrss_fault *out = nullptr)
     return true;
 }
 
-int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
-                      bool pipe = false);
+int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream);
 
-// One set of the lists' workspace (the count matrix zeroed: the parse kernel
-// writes only the columns of the launch)
+// The lists' workspace (the count matrix zeroed: the parse kernel writes only
+// the columns of the launch)
 hipError_t list_ws_alloc(yrss_ctx *c, yrss_ctx::ListWs &w)
 {
     const size_t cnt = (size_t)kMaxChunks * c->nb * sizeof(uint32_t);
@@ -2911,9 +2922,7 @@ hipError_t list_ws_alloc(yrss_ctx *c, yrss_ctx::ListWs &w)
         (e = hipMalloc((void **)&w.totals, c->nb * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc((void **)&w.scan_status, st)) != hipSuccess ||
         (e = hipMemset(w.scan_status, 0, st)) != hipSuccess ||
-        (e = hipMemset(w.seg_cnt, 0, cnt)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&w.parsed, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming)) != hipSuccess)
+        (e = hipMemset(w.seg_cnt, 0, cnt)) != hipSuccess)
         return e;
     return hipSuccess;
 }
@@ -2925,45 +2934,7 @@ void list_ws_free(yrss_ctx::ListWs &w)
     (void)hipFree(w.totals);
     (void)hipFree(w.scan_status);
     (void)hipFree(w.rank);
-    if (w.parsed)
-        (void)hipEventDestroy(w.parsed);
-    if (w.done)
-        (void)hipEventDestroy(w.done);
     w = yrss_ctx::ListWs{};
-}
-
-// Order stream s after every pipelined batch's lists not yet joined.
-int join_lists(yrss_ctx *c, hipStream_t s)
-{
-    for (auto &w : c->ws)
-        if (w.pending) {
-            YRSS_HIP(hipStreamWaitEvent(s, w.done, 0));
-            w.pending = false;
-        }
-    return 0;
-}
-
-// The lists stream of pipelined batches: its own CUs (every eighth CU by
-// default, yrss_tuning.list_cus), so its workgroups never sit on the CUs the
-// next batch's parse kernel is dealt to.
-int lists_stream(yrss_ctx *c)
-{
-    const uint32_t want = c->tune.list_cus ? c->tune.list_cus : (uint32_t)c->cus / 8u;
-    if (c->lstream && c->lstream_cus == want)
-        return 0;
-    if (c->lstream) {
-        YRSS_HIP(hipStreamSynchronize(c->lstream));
-        (void)hipStreamDestroy(c->lstream);
-        c->lstream = nullptr;
-    }
-    std::vector<uint32_t> mask(((uint32_t)c->cus + 31u) / 32u, 0u);
-    const uint32_t step = std::max(1u, (uint32_t)c->cus / want);
-    uint32_t got = 0;
-    for (uint32_t i = step - 1u; i < (uint32_t)c->cus && got < want; i += step, ++got)
-        mask[i / 32u] |= 1u << (i % 32u);
-    YRSS_HIP(hipExtStreamCreateWithCUMask(&c->lstream, (uint32_t)mask.size() * 32u, mask.data()));
-    c->lstream_cus = got;
-    return 0;
 }
 
 bool small_ok(const yrss_ctx *c, uint32_t n)
@@ -3268,7 +3239,7 @@ int yrss_init(const struct yrss_config *cfg, yrss_ctx **out)
     const size_t ws = (size_t)kMaxChunks * c->nb * sizeof(uint32_t);
     hipError_t e;
     (void)ws;
-    if ((e = list_ws_alloc(c, c->ws[0])) != hipSuccess ||
+    if ((e = list_ws_alloc(c, c->ws)) != hipSuccess ||
         (e = hipHostMalloc((void **)&c->d_fault_rec, 64, hipHostMallocCoherent)) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_kni, sizeof(c->kni_bm))) != hipSuccess ||
         (e = hipMalloc((void **)&c->d_fault, sizeof(uint32_t))) != hipSuccess ||
@@ -3326,10 +3297,7 @@ void yrss_fini(yrss_ctx *c)
     for (auto e : c->ev_free)
         (void)hipEventDestroy(e);
     free_burst(c);
-    for (auto &w : c->ws)
-        list_ws_free(w);
-    if (c->lstream)
-        (void)hipStreamDestroy(c->lstream);
+    list_ws_free(c->ws);
     (void)hipHostFree(c->d_fault_rec);
     (void)hipFree(c->d_kni);
     (void)hipFree(c->d_fault);
@@ -3382,37 +3350,11 @@ int yrss_dispatch_dev_ex(yrss_ctx *c, const struct yrss_dev_batch *b, void *stre
     return dispatch_dev_impl(c, b, stream);
 }
 
-int yrss_dispatch_dev_pipelined(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
-{
-    if (!c || !b)
-        return -EINVAL;
-    if (c->pend.active)
-        return -EBUSY;
-    return dispatch_dev_impl(c, b, stream, true);
-}
-
-int yrss_dispatch_join(yrss_ctx *c, void *stream)
-{
-    if (!c)
-        return -EINVAL;
-    return join_lists(c, (hipStream_t)stream);
-}
-
 }  // extern "C"
 
 namespace {
 
-// A pipelined batch's lists are queued: mark the set pending until a join.
-int finish_lists(yrss_ctx *c, yrss_ctx::ListWs &W, bool pipe)
-{
-    if (pipe) {
-        YRSS_HIP(hipEventRecord(W.done, c->lstream));
-        W.pending = true;
-    }
-    return 0;
-}
-
-int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream, bool pipe)
+int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
 {
     const uint32_t n = b->n, win_stride = b->win_stride;
     if (win_stride < YRSS_WIN_MIN || (win_stride & 15u) || n > YRSS_MAX_BATCH)
@@ -3427,10 +3369,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
     if (compact && !b->qstart)
         return -EINVAL;
     hipStream_t s = (hipStream_t)stream;
-    // A batch that is not pipelined uses workspace set 0 on `s` alone: every
-    // pipelined batch's lists come first.
-    if (!pipe && join_lists(c, s) != 0)
-        return -EIO;
     if (n == 0) {
         if (compact)
             YRSS_HIP(hipMemsetAsync(b->qstart, 0, (c->nb + 1) * sizeof(uint32_t), s));
@@ -3448,8 +3386,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
     if (c->last_stream_valid && c->last_stream != s) {
         YRSS_HIP(hipEventRecord(c->switch_ev, c->last_stream));
         YRSS_HIP(hipStreamWaitEvent(s, c->switch_ev, 0));
-        if (join_lists(c, s) != 0)
-            return -EIO;
     }
     c->last_stream = s;
     c->last_stream_valid = true;
@@ -3471,35 +3407,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
         S.qstart = compact ? b->qstart : nullptr;
         return small_launch(c, S, filter, false, s);
     }
-    // pipelined: workspace sets alternate (the set's previous lists must be
-    // done before this parse kernel overwrites it), and the parse kernel
-    // leaves the lists stream's CUs free
-    uint32_t k = 0;
-    if (pipe && compact) {
-        if (lists_stream(c) != 0)
-            return -EIO;
-        k = c->pipe_next;
-        c->pipe_next ^= 1u;
-        auto &w = c->ws[k];
-        if (!w.seg_cnt) {
-            const hipError_t e = list_ws_alloc(c, w);
-            if (e != hipSuccess) {
-                list_ws_free(w);
-                return hip_fail("pipeline workspace", e);
-            }
-            YRSS_HIP(hipDeviceSynchronize());   // the memsets ran on the null stream
-        }
-        if (w.pending) {
-            YRSS_HIP(hipStreamWaitEvent(s, w.done, 0));
-            w.pending = false;
-        }
-    } else {
-        pipe = false;
-    }
-    yrss_ctx::ListWs &W = c->ws[k];
-    uint32_t grid = grid_for(c, n);
-    if (pipe && !c->tune.parse_blocks)
-        grid = std::min(grid, (uint32_t)c->cus - c->lstream_cus);
+    yrss_ctx::ListWs &W = c->ws;
+    const uint32_t grid = grid_for(c, n);
     const Layout lay = layout_for(c, n, grid);
     const uint64_t pwaves = (uint64_t)grid * (kParseBlock / kWave);
     if (compact && ((uint64_t)lay.nchunk + pwaves - 1) / pwaves * c->nb > kCntWords)
@@ -3511,12 +3420,9 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
     const bool ranked = compact && lp.ok && (lp.packed || ((uintptr_t)b->q & 15u) == 0);
     if (ranked && W.rank_cap < n) {
         // the ranks' workspace grows to the largest batch seen; the old one
-        // may still be read by a scatter queued on this stream (or, for a
-        // pipelined set, on the lists stream)
+        // may still be read by a scatter queued on this stream
         if (W.rank) {
             YRSS_HIP(hipStreamSynchronize(s));
-            if (c->lstream)
-                YRSS_HIP(hipStreamSynchronize(c->lstream));
             (void)hipFree(W.rank);
             W.rank = nullptr;
             W.rank_cap = 0;
@@ -3551,12 +3457,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
     YRSS_HIP(hipGetLastError());
     if (!compact)
         return 0;
-    if (pipe) {
-        // the lists of this batch: on the lists stream, after its parse
-        YRSS_HIP(hipEventRecord(W.parsed, s));
-        YRSS_HIP(hipStreamWaitEvent(c->lstream, W.parsed, 0));
-        s = c->lstream;
-    }
     {
         Timed t(c, YRSS_K_SCAN);
         ScanParams SP;
@@ -3600,15 +3500,13 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
         void (*fn)(LineParams) =
             lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
                             : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
-        uint32_t sgrid = resident_blocks(c, (const void *)fn, kLineBlock, lp.lds);
-        if (pipe)   // resident on the lists stream's CUs only
-            sgrid = std::max(1u, sgrid / (uint32_t)c->cus * c->lstream_cus);
-        sgrid = std::min(spans, sgrid);
+        const uint32_t sgrid =
+            std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
         Timed t(c, YRSS_K_SCATTER);
         hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(kLineBlock), lp.lds, s, t.a,
                               t.b, 0, S);
         YRSS_HIP(hipGetLastError());
-        return finish_lists(c, W, pipe);
+        return 0;
     }
     ScatterParams S;
     S.q = b->q;
@@ -3641,7 +3539,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream,
                               t.b, 0, S);
     }
     YRSS_HIP(hipGetLastError());
-    return finish_lists(c, W, pipe);
+    return 0;
 }
 
 }  // namespace
@@ -4589,8 +4487,7 @@ int yrss_set_tuning(yrss_ctx *c, const struct yrss_tuning *t)
     const bool pow2 = (t->chunk_tiles & (t->chunk_tiles - 1u)) == 0 &&
                       (t->span_tiles & (t->span_tiles - 1u)) == 0;
     if (!pow2 || t->chunk_tiles > 4096u || t->span_tiles > 65536u || t->parse_blocks > 65536u ||
-        t->one_launch > 2u || t->scatter_xcd < -1 || t->scatter_xcd > 1 ||
-        t->list_cus > (uint32_t)c->cus / 2u)
+        t->one_launch > 2u || t->scatter_xcd < -1 || t->scatter_xcd > 1)
         return -EINVAL;
     if (c->pend.active)
         return -EBUSY;

@@ -168,11 +168,8 @@ class SoftRss:
     # -- device-resident path ---------------------------------------------
     def dispatch_dev(self, win, lens, stride: int, n: int | None = None, *,
                      out=None, want_hash: bool = True, compact: bool = True,
-                     want_filter: bool = False, stream=None,
-                     pipeline: bool = False) -> DispatchResult:
-        """Classify n packets resident in HBM (``yrss_dispatch_dev_ex``).
-        pipeline=True: ``yrss_dispatch_dev_pipelined`` (the lists are built on
-        the context's lists stream; valid after ``join()`` or a device sync)."""
+                     want_filter: bool = False, stream=None) -> DispatchResult:
+        """Classify n packets resident in HBM (``yrss_dispatch_dev_ex``)."""
         n = int(lens.numel()) if n is None else n
         dev = lens.device
         if out is None:
@@ -180,15 +177,9 @@ class SoftRss:
         _check_dev_sizes(n, stride, win, lens, out, self.nb_queues)
         b = abi.DevBatch(_ptr(win), stride, n, _ptr(lens), _ptr(out.q), _ptr(out.hash),
                          _ptr(out.qidx), _ptr(out.qstart), _ptr(out.filter))
-        fn = self._lib.yrss_dispatch_dev_pipelined if pipeline else self._lib.yrss_dispatch_dev_ex
-        rc = fn(self._ctx, ctypes.byref(b), self._stream(stream))
-        abi.check(rc, "yrss_dispatch_dev_pipelined" if pipeline else "yrss_dispatch_dev_ex")
+        rc = self._lib.yrss_dispatch_dev_ex(self._ctx, ctypes.byref(b), self._stream(stream))
+        abi.check(rc, "yrss_dispatch_dev_ex")
         return out
-
-    def join(self, stream=None) -> None:
-        """Order `stream` after every pipelined batch's lists (yrss_dispatch_join)."""
-        abi.check(self._lib.yrss_dispatch_join(self._ctx, self._stream(stream)),
-                  "yrss_dispatch_join")
 
     def alloc_out(self, n: int, dev, want_hash=True, compact=True,
                   want_filter=False) -> DispatchResult:
@@ -456,10 +447,10 @@ class SoftRss:
         return (int(f.code), int(f.kernel), int(f.where), int(f.value))
 
     def set_tuning(self, chunk_tiles: int = 0, span_tiles: int = 0, parse_blocks: int = 0,
-                   one_launch: int = 0, scatter_xcd: int = -1, list_cus: int = 0) -> None:
+                   one_launch: int = 0, scatter_xcd: int = -1) -> None:
         """Layout overrides for tests and measurements (yrss_set_tuning); the
         results never depend on them."""
-        t = abi.Tuning(chunk_tiles, span_tiles, parse_blocks, one_launch, scatter_xcd, list_cus)
+        t = abi.Tuning(chunk_tiles, span_tiles, parse_blocks, one_launch, scatter_xcd)
         abi.check(self._lib.yrss_set_tuning(self._ctx, ctypes.byref(t)), "yrss_set_tuning")
 
     def grid_for(self, n: int) -> int:
