@@ -266,15 +266,26 @@ def cpu_baseline(args, nb_queues):
     then udp4 and tcp4)."""
     cpus = sorted(os.sched_getaffinity(0))
     share = cpus[: max(1, min(16, len(cpus)))]      # one GPU's share of the box's cores
-    cells = [cpus[:1], share] + ([cpus] if len(cpus) > len(share) else [])
+    cells = [cpus[:1], share]
     profs = list(dict.fromkeys([args.profile, *CPU_PROFILES]))   # the bench's own stream first
-    secs = max(0.5, args.cpu_seconds / (len(cells) * len(profs) * len(CPU_VARIANTS)))
+    secs = max(0.5, args.cpu_seconds / (len(cells) * len(profs) * len(CPU_VARIANTS) + 1))
     by = {}
     for prof in profs:
         by[prof] = {}
         for var in CPU_VARIANTS:
-            by[prof][var] = {str(len(cs)): round(_cpu_run(prof, var, secs, cs), 2)
-                             for cs in cells}
+            by[prof][var] = {}
+            for cs in cells:
+                by[prof][var][str(len(cs))] = round(_cpu_run(prof, var, secs, cs), 2)
+                print(f"cpu_baseline {prof} {var} {len(cs)} cores: "
+                      f"{by[prof][var][str(len(cs))]} Mpkt/s", file=sys.stderr, flush=True)
+    # every core the process may use: the headline cell only (one pinned
+    # process per core; hundreds of interpreter start-ups per cell otherwise)
+    if len(cpus) > len(share):
+        by[args.profile]["bit_serial"][str(len(cpus))] = round(
+            _cpu_run(args.profile, "bit_serial", secs, cpus), 2)
+        print(f"cpu_baseline {args.profile} bit_serial {len(cpus)} cores: "
+              f"{by[args.profile]['bit_serial'][str(len(cpus))]} Mpkt/s", file=sys.stderr,
+              flush=True)
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):

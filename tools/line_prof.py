@@ -52,9 +52,15 @@ def main() -> int:
         spans = used.sum(axis=1)
         d = np.diff(p, axis=2) * 10  # ns
         m = used[:, :, None] & (p[:, :, 1:] != 0) & (p[:, :, :-1] != 0)
+        if blocks == 0:
+            print(f"q{npr}: no spans (one-list batch)")
+            e.close()
+            continue
         print(f"q{npr}: {blocks} workgroups, spans per workgroup {spans.min()}-{spans.max()}")
         for k, name in enumerate(PH):
             v = d[:, :, k][m[:, :, k]]
+            if v.size == 0:
+                continue
             print(f"   {name:20s} mean {v.mean():8.0f} ns  p90 {np.percentile(v, 90):8.0f}")
         first = p[:, 0, 0][used[:, 0]]
         lastidx = spans - 1

@@ -121,7 +121,14 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
                 /* the dispatcher's copy of the burst's windows (cache hot after
                  * rte_eth_rx_burst in F-Stack) is part of the timed work */
                 uint8_t *w = wst + (size_t)k * B * YRSS_WIN_FULL;
+                /* software prefetch 16 windows ahead, into the next burst too
+                 * (the cbench pool is cache-cold, unlike headers just received) */
                 for (uint32_t j = 0; j < B; ++j) {
+                    const uint32_t a = off + j + 16u;
+                    if (a < pool) {
+                        __builtin_prefetch(fdata[a]);
+                        __builtin_prefetch(fdata[a] + 64);
+                    }
                     const uint32_t L = flen[off + j] < YRSS_WIN_FULL ? flen[off + j] : YRSS_WIN_FULL;
                     memcpy(w + (size_t)j * YRSS_WIN_FULL, fdata[off + j], L);
                 }
