@@ -23,8 +23,7 @@ import torch  # noqa: E402
 
 from yastack_amd import SoftRss, abi  # noqa: E402
 
-PH = ["a tab->LDS + S1", "b layout + S2", "c slots/fill/tags", "d place", "prefetch + S4",
-      "e copy-out", "f carry"]
+PH = ["a tab + layout + S1", "b tags/carried/place", "wait + S2", "c copy-out", "d carry"]
 
 
 def main() -> int:
@@ -64,11 +63,11 @@ def main() -> int:
             print(f"   {name:20s} mean {v.mean():8.0f} ns  p90 {np.percentile(v, 90):8.0f}")
         first = p[:, 0, 0][used[:, 0]]
         lastidx = spans - 1
-        ends = np.array([p[b, lastidx[b], 7] for b in range(2048) if used[b, 0]])
+        ends = np.array([p[b, lastidx[b], len(PH)] for b in range(2048) if used[b, 0]])
         t0 = first.min()
         print(f"   workgroup start spread {(first.max() - t0) * 10:.0f} ns, "
               f"end {(ends.min() - t0) * 10:.0f}-{(ends.max() - t0) * 10:.0f} ns after the first start")
-        per_span = (p[:, :, 7] - p[:, :, 0])[used] * 10
+        per_span = (p[:, :, len(PH)] - p[:, :, 0])[used] * 10
         print(f"   span total mean {per_span.mean():.0f} ns")
         e.close()
     return 0

@@ -1141,21 +1141,33 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
 // The packets' (bucket, rank) come from the parse kernel's rank stream: packed
 // as bucket << cshift | rank when the bucket fits beside the rank (kPacked;
 // the scatter then reads 2 bytes a packet), else the rank beside q.  Checks: a
-// slot outside the stage lands in a spare word, every stage word is
-// pre-filled with 0xFFFFFFFF and a list word still holding it is a hole
-// (two packets on one slot), and the words a workgroup writes must add up to
-// its range's packets; each reports through the fault record instead of
-// storing (YRSS_FAULT_STAGE / _LIST_RANGE / _COUNT_MISMATCH).
+// slot outside the stage lands in a spare word, a list position outside the
+// batch is not stored, and the words a workgroup writes must add up to its
+// range's packets with the sum of its range's packet indices (two packets on
+// one slot leave another slot holding an earlier span's index); each reports
+// through the fault record instead of storing (YRSS_FAULT_STAGE /
+// _LIST_RANGE / _COUNT_MISMATCH).
 // ---------------------------------------------------------------------------
 constexpr int kLineBlock = 512;
-constexpr uint32_t kLineTabRegs = 9;                     // prefix words a thread
-constexpr uint32_t kLineTabMax = kLineBlock * kLineTabRegs;  // nb x span chunks <= 4608
+// s_waitcnt vmcnt(0), expcnt and lgkmcnt left alone (gfx9 encoding)
+constexpr int kWaitVm0 = 0x0F70;
+#ifndef YRSS_SL_ISSUE
+#define YRSS_SL_ISSUE 2
+#endif
+// where a span issues the next span's loads: 0 after its place phase, 1 after
+// its prefixes went to LDS, 2 before its tagging phase (1 and 2 wait for them
+// before the copy-out)
+constexpr int kSlIssue = YRSS_SL_ISSUE;
+// prefix words a thread holds: the table is nb x span chunks <= 512 x regs
+// words (2048 at default chunks: 128 buckets x 16 chunks; more only when
+// chunk_tiles is forced small, where the span gets fewer chunks instead)
+constexpr uint32_t line_tab_regs(uint32_t g) { return g == 2u ? 5u : 9u; }
+constexpr uint32_t line_tab_max(uint32_t g) { return kLineBlock * line_tab_regs(g); }
 // A span is kG 8-packet groups a thread: 8192 packets (kG = 2) up to 128
 // buckets, 16384 (kG = 4) past that, where the per-bucket work of a span
 // (carried lines, layout) is large enough to amortise over twice the packets
 // (q255 scatter 93 -> 75 us; at 64 buckets kG = 4 cost 3-4 us, r03 A/B).
 constexpr uint32_t line_span_max(uint32_t g) { return kLineBlock * 8u * g; }
-constexpr uint32_t kHole = 0xFFFFFFFFu;
 
 
 struct LineParams {
@@ -1176,7 +1188,7 @@ struct LineParams {
 // LDS of a workgroup, in words: per-bucket arrays, the prefix table, the
 // carried lines, the stage's line tags, the stage (+ a spare word).
 struct LineLds {
-    uint32_t start, cs, ve, ce, so, rb, tend, lsl, misc, tab, cb, ltag, lgl, stg, words;
+    uint32_t start, cs, ve, ce, so, rb, lsl, misc, tab, cb, ltag, lgl, stg, words;
 };
 __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32_t lmax)
 {
@@ -1193,7 +1205,6 @@ __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32
     L.ce = take(nb);      // carry end = the span's first packet position (adjusted)
     L.so = take(nb);      // stage index = so[b] + adjusted position
     L.rb = take(nb);      // prefix table row bias (to stage slots)
-    L.tend = take(nb);    // prefix at the span's end
     L.lsl = take(nb + 1u);   // first stage line of each bucket
     L.misc = take(4);
     L.tab = take(nb * ((1u << gshift) + 1u));   // rows of 2^gshift + 1 words (odd: banks)
@@ -1259,7 +1270,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t / kWave);
     const LineLds o = line_lds(nb, P.gshift, P.lmax);
     uint32_t *start = lsm + o.start, *cs = lsm + o.cs, *ve = lsm + o.ve, *ce = lsm + o.ce;
-    uint32_t *so = lsm + o.so, *rb = lsm + o.rb, *tend = lsm + o.tend, *lsl = lsm + o.lsl;
+    uint32_t *so = lsm + o.so, *rb = lsm + o.rb, *lsl = lsm + o.lsl;
     uint32_t *misc = lsm + o.misc, *tab = lsm + o.tab, *cb = lsm + o.cb, *ltag = lsm + o.ltag;
     uint32_t *lgl = lsm + o.lgl;
     uint32_t *stg = lsm + o.stg;
@@ -1337,73 +1348,106 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         ve[b] = a;
     }
     const ListOut lout = list_out(P.qidx, P.n);
-    u32x4 pk[kG], qk[kG];
-    uint32_t pt[kLineTabRegs], pend = 0;
-    auto load_span = [&](uint32_t g) {
+    // The span's streams alternate between two register sets: span g+1's
+    // loads issue at the start of span g, right after its prefixes went to
+    // LDS, and are waited for just before span g's copy-out.  vmcnt counts
+    // loads and stores in one in-order queue, so a load issued before a
+    // span's list stores and waited for after them waits for those stores
+    // too (their write-through acks), and a load issued after the place phase
+    // had only the copy-out to hide its latency.
+    u32x4 pkA[kG], qkA[kG], pkB[kG], qkB[kG];
+    // wave 0 also holds, a bucket to a lane, each bucket's prefix at the
+    // span's first chunk and at its end, so it lays the span out from
+    // registers while the other waves write the prefix table
+    constexpr uint32_t kBI = kG == 2u ? 2u : 8u;   // nb <= 64 kBI
+    constexpr uint32_t kLineTabRegs = line_tab_regs(kG);
+    uint32_t pt[kLineTabRegs], w0s[kBI], w0e[kBI];
+    auto load_span = [&](uint32_t g, u32x4 (&pk)[kG], u32x4 (&qk)[kG]) {
         const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
         load_groups(P.rank, p0, pe, tt, pk);
         if (!kPacked)
             load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, qk);
         const uint32_t c0 = g << P.gshift;
-        if (c0 + ncs < P.nchunk) {
-            // every column of the span and the next span's first are counts:
-            // element k * 512 + t is row (t >> gshift) + k * (512 >> gshift),
-            // column t & (ncs - 1), so one per-lane offset and a scalar step
-            // per k; rows past nb read 0 (range check)
-            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        if (wave == 0) {
+            // rows past nb read 0 (range check); a span's end past the last
+            // chunk is the bucket's total
+            const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
-            const uint32_t vo = ((tt >> P.gshift) * P.ncol + (tt & (ncs - 1u))) * 4u;
-            const uint32_t step = (kLineBlock >> P.gshift) * P.ncol * 4u;
+            const __amdgpu_buffer_rsrc_t rtot = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint32_t *>(P.totals), 0, (int)(nb * 4u), kRsrcWord3);
+            const bool inner = c0 + ncs < P.nchunk;
+            const uint32_t ll = opaque(lane);
 #pragma unroll
-            for (uint32_t k = 0; k < kLineTabRegs; ++k)
-                if (k * kLineBlock < ntab)   // (uniform)
-                    pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo,
-                                                                 (int)(c0 * 4u + k * step), 0);
-            pend = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(tt * P.ncol * 4u),
-                                                        (int)((c0 + ncs) * 4u), 0);
-        } else {
-#pragma unroll
-            for (uint32_t k = 0; k < kLineTabRegs; ++k) {
-                const uint32_t e = k * kLineBlock + tt;
-                pt[k] = e < ntab ? prefix(e >> P.gshift, c0 + (e & (ncs - 1u))) : 0u;
+            for (uint32_t i = 0; i < kBI; ++i) {
+                if (i * kWave < nb) {   // (uniform)
+                    const uint32_t b = i * kWave + ll;
+                    w0s[i] = __builtin_amdgcn_raw_buffer_load_b32(rs0, (int)(b * P.ncol * 4u),
+                                                                  (int)(c0 * 4u), 0);
+                    w0e[i] = inner ? __builtin_amdgcn_raw_buffer_load_b32(
+                                         rs0, (int)(b * P.ncol * 4u), (int)((c0 + ncs) * 4u), 0)
+                                   : __builtin_amdgcn_raw_buffer_load_b32(rtot, (int)(b * 4u), 0, 0);
+                }
             }
-            if (tt < nb)
-                pend = prefix(tt, c0 + ncs);
         }
+        // element k * 512 + t is row (t >> gshift) + k * (512 >> gshift),
+        // column t & (ncs - 1), so one per-lane offset and a scalar step per
+        // k; rows past nb read 0 (range check).  Columns past the last chunk
+        // (a batch's last span) read whatever the matrix holds there: no
+        // packet's slot uses them.  One load form on every path: a plain
+        // load on a rare path left a pending destination register that the
+        // compiler later waited for with vmcnt(0), i.e. for every list store
+        // in flight.
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
+        const uint32_t vo = ((tt >> P.gshift) * P.ncol + (tt & (ncs - 1u))) * 4u;
+        const uint32_t step = (kLineBlock >> P.gshift) * P.ncol * 4u;
+#pragma unroll
+        for (uint32_t k = 0; k < kLineTabRegs; ++k)
+            if (k * kLineBlock < ntab)   // (uniform)
+                pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo,
+                                                             (int)(c0 * 4u + k * step), 0);
     };
-    load_span(g0);
+    load_span(g0, pkA, qkA);
+    // the first span's loads waited for here, so that at the loop head no
+    // load is pending on any path: a pending one there made the compiler wait
+    // vmcnt(0) at the prefix table's first use in every span, i.e. for the
+    // previous span's list stores as well
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
     // words written and their sum: a range is complete iff it wrote each of
     // its packets once, so the sum must be that of its packet indices (two
     // packets on one slot leave another slot with an earlier span's index)
     uint32_t wrote = 0, wsum = 0;
-    for (uint32_t g = g0; g < g1; ++g) {
+    // the thread's bucket and line slice in the tagging phase
+    const uint32_t tk = kLineBlock / nb, tb = t % nb, tj = t / nb;
+    auto span = [&](uint32_t g, const u32x4 (&pk)[kG], const u32x4 (&qk)[kG], u32x4 (&pkn)[kG],
+                    u32x4 (&qkn)[kG]) {
         const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
         const bool last = g + 1u == g1;
         LPROF(0);
-        // (a) the span's prefixes: tab[b][c] at chunk c, tend[b] at its end
+        // (a) every thread: its prefix words into the table, tab[b][c] at
+        // chunk c (rows of ncs + 1 words); then the next span's loads.
+        // Wave 0 meanwhile, a bucket to a lane, from the prefixes it holds:
+        // the valid positions [cs, ve) = the carried words and the span's
+        // packets, the bucket's stage lines (exclusive scan), its stage offset
+        // so and the bias rb from a prefix to a stage slot.
 #pragma unroll
         for (uint32_t k = 0; k < kLineTabRegs; ++k) {
             const uint32_t e = k * kLineBlock + t;
             if (k * kLineBlock < ntab && e < ntab)
                 tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k];
         }
-        if (t < nb)
-            tend[t] = pend;
-        __syncthreads();
-        LPROF(1);
-        // (b) per bucket: the valid positions [cs, ve) = the carried words and
-        // the span's packets; its stage lines (exclusive scan), stage offset
-        // and the prefix rows' bias
         if (wave == 0) {
             uint32_t lines = 0;
-            for (uint32_t b0 = 0; b0 < nb; b0 += kWave) {
-                const uint32_t b = b0 + lane;
-                uint32_t nl = 0, v0 = 0, t0 = 0, e0 = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < kBI; ++i) {
+                if (i * kWave >= nb)   // (uniform)
+                    break;
+                const uint32_t b = i * kWave + lane;
+                uint32_t nl = 0, v0 = 0, e0 = 0;
                 if (b < nb) {
                     e0 = ve[b];
                     v0 = max(cs[b], e0 & ~15u);
-                    t0 = tab[b * rs];
-                    const uint32_t e1 = e0 + (tend[b] - t0);
+                    const uint32_t e1 = e0 + (w0e[i] - w0s[i]);
                     cs[b] = v0;
                     ce[b] = e0;
                     ve[b] = e1;
@@ -1414,7 +1458,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                     const uint32_t l0 = lines + x - nl;
                     lsl[b] = l0;
                     so[b] = 16u * (l0 - (v0 >> 4));
-                    rb[b] = 16u * (l0 - (v0 >> 4)) + e0 - t0;
+                    rb[b] = 16u * (l0 - (v0 >> 4)) + e0 - w0s[i];
                 }
                 lines += __shfl(x, kWave - 1, kWave);
             }
@@ -1427,32 +1471,33 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 misc[2] = lines;
             }
         }
+        if (kSlIssue == 1 && !last)
+            load_span(g + 1u, pkn, qkn);
         __syncthreads();
-        LPROF(2);
+        LPROF(1);
         const uint32_t L = __builtin_amdgcn_readfirstlane(misc[2]);
-        // (c) prefix rows -> stage slots; each stage line tagged with its
-        // bucket, list line and copy mode (0 whole, 1 carried, 2 word by word)
-        for (uint32_t e = t; e < ntab; e += kLineBlock)
-            tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] += rb[e >> P.gshift];
-        for (uint32_t l = t; l < L; l += kLineBlock) {
-            uint32_t lo = 0, hi = nb;   // lsl[lo] <= l < lsl[hi]
-            while (hi - lo > 1u) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (lsl[mid] <= l)
-                    lo = mid;
-                else
-                    hi = mid;
+        // (b) three independent writes into LDS, no barrier between them:
+        // - each stage line tagged with its bucket, list line and copy mode
+        //   (0 whole, 1 carried, 2 word by word): thread t tags lines tj,
+        //   tj + tk, ... of bucket tb (tk = 512 / nb threads to a bucket), one
+        //   read of the bucket's bounds, then stores (a per-line binary search
+        //   over the buckets' first lines was a chain of log2 nb dependent LDS
+        //   reads; a wave per bucket walked nb / 8 buckets in turn);
+        // - the carried words into their stage slots;
+        // - every packet at slot = tab[b][chunk] + rb[b] + rank.
+        if (kSlIssue == 2 && !last)
+            load_span(g + 1u, pkn, qkn);
+        if (tj < tk) {
+            const uint32_t l0 = lsl[tb], l1 = L ? lsl[tb + 1u] : 0u, v0 = cs[tb], e1 = ve[tb];
+            for (uint32_t l = l0 + tj; l < l1; l += tk) {
+                const uint32_t gl = l - l0 + (v0 >> 4);
+                const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
+                                      : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
+                                                                                      : 2u;
+                ltag[l] = tb | mode << 30;
+                lgl[l] = gl;
             }
-            const uint32_t v0 = cs[lo], e1 = ve[lo], gl = l - lsl[lo] + (v0 >> 4);
-            const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
-                                  : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
-                                                                                  : 2u;
-            ltag[l] = lo | mode << 30;
-            lgl[l] = gl;
         }
-        __syncthreads();
-        LPROF(3);
-        // (d) the carried words, then every packet at its slot
         for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
             const uint32_t b = e >> 4, j = e & 15u;
             if (j < ce[b] - cs[b])
@@ -1485,7 +1530,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                                       P.nq);
                         rk = w;
                     }
-                    slot[k - k0][j] = tab[__umul24(b, rs) + cc] + rk;
+                    slot[k - k0][j] = tab[__umul24(b, rs) + cc] + rb[b] + rk;
                 }
             }
 #pragma unroll
@@ -1503,13 +1548,17 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             place(std::false_type{});
         else
             place(std::true_type{});
-        // the next span's streams and prefixes are in flight during the copy-out
-        LPROF(4);
-        if (!last)
-            load_span(g + 1u);
+        LPROF(2);
+        if (kSlIssue == 0 && !last)
+            load_span(g + 1u, pkn, qkn);
+        // the next span's streams and prefixes (issued in (a)) have arrived;
+        // waiting here, before this span's list stores, keeps those stores
+        // out of the next wait (vmcnt counts loads and stores in one queue)
+        if (kSlIssue != 0)
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
         __syncthreads();
-        LPROF(5);
-        // (e) copy-out, a quad per thread: whole lines as 16-byte non-temporal
+        LPROF(3);
+        // (c) copy-out, a quad per thread: whole lines as 16-byte non-temporal
         // stores; the bucket's last line, if the span ends inside it, is
         // carried (unless the range ends here); partial lines word by word
         auto copy_quad = [&](uint32_t v, uint32_t tag, uint32_t gl, const u32x4 &e) {
@@ -1564,8 +1613,8 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             for (uint32_t i = 0; i < kCopyQ; ++i)
                 copy_quad(v0 + i * kLineBlock, tg[i], gl[i], eq[i]);
         }
-        LPROF(6);
-        // (f) carry the unfinished last lines
+        LPROF(4);
+        // (d) carry the unfinished last lines
         if (!last) {
             for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
                 const uint32_t b = e >> 4, j = e & 15u;
@@ -1573,8 +1622,15 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 if (j < e1 - nv)
                     cb[e] = stg[min(so[b] + nv + j, cap)];
             }
+            // the next span's (a) rewrites the per-bucket arrays read above
+            __syncthreads();
         }
-        LPROF(7);
+        LPROF(5);
+    };
+    for (uint32_t g = g0; g < g1; g += 2u) {
+        span(g, pkA, qkA, pkB, qkB);
+        if (g + 1u < g1)
+            span(g + 1u, pkB, qkB, pkA, qkA);
     }
     // every packet of the range left exactly once
     wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
@@ -2612,7 +2668,7 @@ ScatterLds scatter_lds(uint32_t nb)
 
 // The line scatter's span and stage for a layout: spans of up to
 // kLineSpanMax packets (yrss_tuning.span_tiles lowers it), as many chunks as
-// keep the prefix table within kLineTabMax words; none when a chunk is longer
+// keep the prefix table within line_tab_max words; none when a chunk is longer
 // than a span can be (batches past ~2^29 packets) or the LDS would not fit.
 struct LinePlan {
     bool ok, packed;
@@ -2631,9 +2687,9 @@ LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
     target = std::min<uint64_t>(std::max<uint64_t>(target, lay.chunk), smax);
     p.gshift = 0;
     while (((uint64_t)lay.chunk << (p.gshift + 1)) <= target &&
-           ((uint64_t)nb << (p.gshift + 1)) <= kLineTabMax)
+           ((uint64_t)nb << (p.gshift + 1)) <= line_tab_max(p.groups))
         ++p.gshift;
-    if (((uint64_t)nb << p.gshift) > kLineTabMax)
+    if (((uint64_t)nb << p.gshift) > line_tab_max(p.groups))
         return p;
     p.seg = lay.chunk << p.gshift;
     p.lmax = p.seg / 16u + 2u * nb + 1u;   // a bucket's lines <= (its packets + 30) / 16
