@@ -1151,13 +1151,6 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
 constexpr int kLineBlock = 512;
 // s_waitcnt vmcnt(0), expcnt and lgkmcnt left alone (gfx9 encoding)
 constexpr int kWaitVm0 = 0x0F70;
-#ifndef YRSS_SL_ISSUE
-#define YRSS_SL_ISSUE 2
-#endif
-// where a span issues the next span's loads: 0 after its place phase, 1 after
-// its prefixes went to LDS, 2 before its tagging phase (1 and 2 wait for them
-// before the copy-out)
-constexpr int kSlIssue = YRSS_SL_ISSUE;
 // prefix words a thread holds: the table is nb x span chunks <= 512 x regs
 // words (2048 at default chunks: 128 buckets x 16 chunks; more only when
 // chunk_tiles is forced small, where the span gets fewer chunks instead)
@@ -1199,14 +1192,15 @@ __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32
         o = (o + w + 3u) & ~3u;
         return at;
     };
+    // the per-bucket layout arrays come in two sets, a span's and the next's
     L.start = take(nb);
-    L.cs = take(nb);      // this span's first valid list position (adjusted), carry start
-    L.ve = take(nb);      // this span's end position (adjusted)
-    L.ce = take(nb);      // carry end = the span's first packet position (adjusted)
-    L.so = take(nb);      // stage index = so[b] + adjusted position
-    L.rb = take(nb);      // prefix table row bias (to stage slots)
-    L.lsl = take(nb + 1u);   // first stage line of each bucket
-    L.misc = take(4);
+    L.cs = take(2u * nb);    // the span's first valid list position (adjusted), carry start
+    L.ve = take(2u * nb);    // the span's end position (adjusted)
+    L.ce = take(2u * nb);    // carry end = the span's first packet position (adjusted)
+    L.so = take(2u * nb);    // stage index = so[b] + adjusted position
+    L.rb = take(2u * nb);    // prefix table row bias (to stage slots)
+    L.lsl = take(2u * (nb + 1u));   // first stage line of each bucket
+    L.misc = take(8);
     L.tab = take(nb * ((1u << gshift) + 1u));   // rows of 2^gshift + 1 words (odd: banks)
     L.cb = take(16u * nb);
     L.ltag = take(lmax);  // bucket | copy mode << 30 per stage line
@@ -1274,6 +1268,8 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     uint32_t *misc = lsm + o.misc, *tab = lsm + o.tab, *cb = lsm + o.cb, *ltag = lsm + o.ltag;
     uint32_t *lgl = lsm + o.lgl;
     uint32_t *stg = lsm + o.stg;
+    uint32_t *const cs_sets = cs, *const ve_sets = ve, *const ce_sets = ce, *const so_sets = so;
+    uint32_t *const rb_sets = rb, *const lsl_sets = lsl;
     const uint32_t cap = 16u * P.lmax;   // the spare word
     // list position x is "adjusted" a = x + ph: 64-byte lines are a >> 4
     const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 15u);
@@ -1342,14 +1338,15 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         const uint64_t e = (uint64_t)g * P.seg + P.seg;
         return e < P.n ? (uint32_t)e : P.n;
     };
+    // set 1 holds the state before the range's first span (set 0)
     for (uint32_t b = t; b < nb; b += kLineBlock) {
         const uint32_t a = start[b] + prefix(b, g0 << P.gshift) + ph;
-        cs[b] = a;
-        ve[b] = a;
+        cs[nb + b] = a;
+        ve[nb + b] = a;
     }
     const ListOut lout = list_out(P.qidx, P.n);
     // The span's streams alternate between two register sets: span g+1's
-    // loads issue at the start of span g, right after its prefixes went to
+    // loads issue at the start of span g's phase (b), once its table is in
     // LDS, and are waited for just before span g's copy-out.  vmcnt counts
     // loads and stores in one in-order queue, so a load issued before a
     // span's list stores and waited for after them waits for those stores
@@ -1413,69 +1410,83 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // vmcnt(0) at the prefix table's first use in every span, i.e. for the
     // previous span's list stores as well
     __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    // Wave 0, a bucket to a lane, lays span g out into set s from set s ^ 1
+    // and the prefixes it holds (w0s, w0e): the valid positions [cs, ve) =
+    // the carried words and the span's packets, the bucket's stage lines
+    // (exclusive scan), its stage offset so and the bias rb from a prefix to
+    // a stage slot.  Span g + 1's layout is made during span g's copy-out,
+    // so a span starts with its layout in place.
+    auto layout = [&](uint32_t g, uint32_t s) {
+        const uint32_t *pcs = cs + (s ^ 1u) * nb, *pve = ve + (s ^ 1u) * nb;
+        uint32_t *wcs = cs + s * nb, *wve = ve + s * nb, *wce = ce + s * nb, *wso = so + s * nb;
+        uint32_t *wrb = rb + s * nb, *wlsl = lsl + s * (nb + 1u);
+        uint32_t lines = 0;
+        // (lane hidden from the optimiser: the per-lane LDS addresses of
+        // both sets were hoisted out of the span loop and spilled)
+        const uint32_t ll = opaque(lane);
+#pragma unroll
+        for (uint32_t i = 0; i < kBI; ++i) {
+            if (i * kWave >= nb)   // (uniform)
+                break;
+            const uint32_t b = i * kWave + ll;
+            uint32_t nl = 0, v0 = 0, e0 = 0;
+            if (b < nb) {
+                e0 = pve[b];
+                v0 = max(pcs[b], e0 & ~15u);
+                const uint32_t e1 = e0 + (w0e[i] - w0s[i]);
+                wcs[b] = v0;
+                wce[b] = e0;
+                wve[b] = e1;
+                nl = ((e1 + 15u) >> 4) - (v0 >> 4);
+            }
+            const uint32_t x = wave_incl_scan(nl, lane);
+            if (b < nb) {
+                const uint32_t l0 = lines + x - nl;
+                wlsl[b] = l0;
+                wso[b] = 16u * (l0 - (v0 >> 4));
+                wrb[b] = 16u * (l0 - (v0 >> 4)) + e0 - w0s[i];
+            }
+            lines += __shfl(x, kWave - 1, kWave);
+        }
+        if (lane == 0) {
+            if (lines > P.lmax) {
+                report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g, lines);
+                lines = 0;
+            }
+            wlsl[nb] = lines;
+            misc[4u + s] = lines;
+        }
+    };
+    __syncthreads();   // set 1 written
+    if (wave == 0)
+        layout(g0, 0u);
+    __syncthreads();
     // words written and their sum: a range is complete iff it wrote each of
     // its packets once, so the sum must be that of its packet indices (two
     // packets on one slot leave another slot with an earlier span's index)
     uint32_t wrote = 0, wsum = 0;
     // the thread's bucket and line slice in the tagging phase
     const uint32_t tk = kLineBlock / nb, tb = t % nb, tj = t / nb;
-    auto span = [&](uint32_t g, const u32x4 (&pk)[kG], const u32x4 (&qk)[kG], u32x4 (&pkn)[kG],
-                    u32x4 (&qkn)[kG]) {
+    auto span = [&](uint32_t g, uint32_t s, const u32x4 (&pk)[kG], const u32x4 (&qk)[kG],
+                    u32x4 (&pkn)[kG], u32x4 (&qkn)[kG]) {
         const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
         const bool last = g + 1u == g1;
+        const uint32_t *cs = cs_sets + s * nb, *ve = ve_sets + s * nb, *ce = ce_sets + s * nb;
+        const uint32_t *so = so_sets + s * nb, *rb = rb_sets + s * nb;
+        const uint32_t *lsl = lsl_sets + s * (nb + 1u);
         LPROF(0);
-        // (a) every thread: its prefix words into the table, tab[b][c] at
-        // chunk c (rows of ncs + 1 words); then the next span's loads.
-        // Wave 0 meanwhile, a bucket to a lane, from the prefixes it holds:
-        // the valid positions [cs, ve) = the carried words and the span's
-        // packets, the bucket's stage lines (exclusive scan), its stage offset
-        // so and the bias rb from a prefix to a stage slot.
+        // (a) every thread: its prefix words into the table with their row's
+        // bias, tab[b][c] = prefix at chunk c + rb[b] (rows of ncs + 1
+        // words): a packet's stage slot is then tab[b][chunk] + rank
 #pragma unroll
         for (uint32_t k = 0; k < kLineTabRegs; ++k) {
             const uint32_t e = k * kLineBlock + t;
             if (k * kLineBlock < ntab && e < ntab)
-                tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k];
+                tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k] + rb[e >> P.gshift];
         }
-        if (wave == 0) {
-            uint32_t lines = 0;
-#pragma unroll
-            for (uint32_t i = 0; i < kBI; ++i) {
-                if (i * kWave >= nb)   // (uniform)
-                    break;
-                const uint32_t b = i * kWave + lane;
-                uint32_t nl = 0, v0 = 0, e0 = 0;
-                if (b < nb) {
-                    e0 = ve[b];
-                    v0 = max(cs[b], e0 & ~15u);
-                    const uint32_t e1 = e0 + (w0e[i] - w0s[i]);
-                    cs[b] = v0;
-                    ce[b] = e0;
-                    ve[b] = e1;
-                    nl = ((e1 + 15u) >> 4) - (v0 >> 4);
-                }
-                const uint32_t x = wave_incl_scan(nl, lane);
-                if (b < nb) {
-                    const uint32_t l0 = lines + x - nl;
-                    lsl[b] = l0;
-                    so[b] = 16u * (l0 - (v0 >> 4));
-                    rb[b] = 16u * (l0 - (v0 >> 4)) + e0 - w0s[i];
-                }
-                lines += __shfl(x, kWave - 1, kWave);
-            }
-            if (lane == 0) {
-                if (lines > P.lmax) {
-                    report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g, lines);
-                    lines = 0;
-                }
-                lsl[nb] = lines;
-                misc[2] = lines;
-            }
-        }
-        if (kSlIssue == 1 && !last)
-            load_span(g + 1u, pkn, qkn);
         __syncthreads();
         LPROF(1);
-        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[2]);
+        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + s]);
         // (b) three independent writes into LDS, no barrier between them:
         // - each stage line tagged with its bucket, list line and copy mode
         //   (0 whole, 1 carried, 2 word by word): thread t tags lines tj,
@@ -1484,17 +1495,18 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         //   over the buckets' first lines was a chain of log2 nb dependent LDS
         //   reads; a wave per bucket walked nb / 8 buckets in turn);
         // - the carried words into their stage slots;
-        // - every packet at slot = tab[b][chunk] + rb[b] + rank.
-        if (kSlIssue == 2 && !last)
+        // - every packet at slot = tab[b][chunk] + rank.
+        if (!last)
             load_span(g + 1u, pkn, qkn);
         if (tj < tk) {
-            const uint32_t l0 = lsl[tb], l1 = L ? lsl[tb + 1u] : 0u, v0 = cs[tb], e1 = ve[tb];
+            const uint32_t b = opaque(tb);   // (addresses not hoisted: registers)
+            const uint32_t l0 = lsl[b], l1 = L ? lsl[b + 1u] : 0u, v0 = cs[b], e1 = ve[b];
             for (uint32_t l = l0 + tj; l < l1; l += tk) {
                 const uint32_t gl = l - l0 + (v0 >> 4);
                 const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
                                       : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
                                                                                       : 2u;
-                ltag[l] = tb | mode << 30;
+                ltag[l] = b | mode << 30;
                 lgl[l] = gl;
             }
         }
@@ -1530,7 +1542,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                                       P.nq);
                         rk = w;
                     }
-                    slot[k - k0][j] = tab[__umul24(b, rs) + cc] + rb[b] + rk;
+                    slot[k - k0][j] = tab[__umul24(b, rs) + cc] + rk;
                 }
             }
 #pragma unroll
@@ -1549,13 +1561,10 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         else
             place(std::true_type{});
         LPROF(2);
-        if (kSlIssue == 0 && !last)
-            load_span(g + 1u, pkn, qkn);
-        // the next span's streams and prefixes (issued in (a)) have arrived;
+        // the next span's streams and prefixes (issued in (b)) have arrived;
         // waiting here, before this span's list stores, keeps those stores
         // out of the next wait (vmcnt counts loads and stores in one queue)
-        if (kSlIssue != 0)
-            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
         __syncthreads();
         LPROF(3);
         // (c) copy-out, a quad per thread: whole lines as 16-byte non-temporal
@@ -1593,13 +1602,19 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         };
         // kCopyQ quads a turn, all loaded before any is stored (an
         // 8192-packet span's lines fit one turn up to ~128 buckets)
-        constexpr uint32_t kCopyQ = 5u;
-        for (uint32_t v0 = t; v0 < 4u * L; v0 += kCopyQ * kLineBlock) {
+        // Wave 0 first lays out the next span (its loads were waited for
+        // above), then takes its share of the copy-out (leaving the copy-out
+        // to the other seven waves was no faster: the copy-out is bound by
+        // the stores, profiles/r03_h9_ab_copyall.log).
+        constexpr uint32_t kCopyQ = 5u, nct = kLineBlock;
+        if (!last && wave == 0)
+            layout(g + 1u, s ^ 1u);
+        for (uint32_t v0 = t; v0 < 4u * L; v0 += kCopyQ * nct) {
             uint32_t tg[kCopyQ], gl[kCopyQ];
             u32x4 eq[kCopyQ];
 #pragma unroll
             for (uint32_t i = 0; i < kCopyQ; ++i) {
-                const uint32_t v = v0 + i * kLineBlock;
+                const uint32_t v = v0 + i * nct;
                 tg[i] = 1u << 30;   // mode 1: nothing to store
                 gl[i] = 0u;
                 eq[i] = u32x4{0u, 0u, 0u, 0u};
@@ -1611,7 +1626,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             }
 #pragma unroll
             for (uint32_t i = 0; i < kCopyQ; ++i)
-                copy_quad(v0 + i * kLineBlock, tg[i], gl[i], eq[i]);
+                copy_quad(v0 + i * nct, tg[i], gl[i], eq[i]);
         }
         LPROF(4);
         // (d) carry the unfinished last lines
@@ -1628,9 +1643,9 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         LPROF(5);
     };
     for (uint32_t g = g0; g < g1; g += 2u) {
-        span(g, pkA, qkA, pkB, qkB);
+        span(g, 0u, pkA, qkA, pkB, qkB);
         if (g + 1u < g1)
-            span(g + 1u, pkB, qkB, pkA, qkA);
+            span(g + 1u, 1u, pkB, qkB, pkA, qkA);
     }
     // every packet of the range left exactly once
     wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
