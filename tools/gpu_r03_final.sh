@@ -36,5 +36,8 @@ fi
 # PART=a stops here (the set in two gpurun calls: PART=a, then PART=b)
 [ "${PART:-all}" = a ] && { echo "== done (part a)"; exit 0; }
 bash tools/gpu_r03_qrows.sh r03 || exit 1
+if [ -f ab/lib/libyrss_prof7.so ]; then   # the line scatter's phase clock (a YRSS_PROF_LINES build)
+    step lineprof 200 python tools/line_prof.py --lib ab/lib/libyrss_prof7.so --nb-procs 3,8,64,255 || exit 1
+fi
 bash tools/gpu_pmc.sh r03 "3 8 64 255" || exit 1
 echo "== done"
