@@ -26,13 +26,14 @@ CONFIGS = [
     ("-", "tcp4", "64B TCP/IPv4, 1M flows (all hashed)", []),
 ]
 # the same all-hashed stream over more dispatch queues (nb_procs lcores,
-# dispatch_only_core): each scatter path in turn (yrss.hip)
+# dispatch_only_core): the line scatter at 8192-packet spans up to 128
+# buckets (packed ranks), 16 384-packet spans beyond (yrss.hip)
 QUEUES = [
-    ("q8", "tcp4", "64B TCP/IPv4, nb_procs 8 (9 buckets: ranked, group stage)", ["--nb-procs", "8"]),
-    ("q16", "tcp4", "64B TCP/IPv4, nb_procs 16 (17 buckets: ranked, group stage, XCD-contiguous groups)", ["--nb-procs", "16"]),
-    ("q32", "tcp4", "64B TCP/IPv4, nb_procs 32 (33 buckets: ranked, group stage, XCD-contiguous groups)", ["--nb-procs", "32"]),
-    ("q64", "tcp4", "64B TCP/IPv4, nb_procs 64 (65 buckets: ranked, group stage, XCD-contiguous groups)", ["--nb-procs", "64"]),
-    ("q255", "tcp4", "64B TCP/IPv4, nb_procs 255 (256 buckets: ranked, group stage, XCD-contiguous groups)", ["--nb-procs", "255"]),
+    ("q8", "tcp4", "64B TCP/IPv4, nb_procs 8 (9 buckets)", ["--nb-procs", "8"]),
+    ("q16", "tcp4", "64B TCP/IPv4, nb_procs 16 (17 buckets)", ["--nb-procs", "16"]),
+    ("q32", "tcp4", "64B TCP/IPv4, nb_procs 32 (33 buckets)", ["--nb-procs", "32"]),
+    ("q64", "tcp4", "64B TCP/IPv4, nb_procs 64 (65 buckets)", ["--nb-procs", "64"]),
+    ("q255", "tcp4", "64B TCP/IPv4, nb_procs 255 (256 buckets, 16 384-packet spans, rank beside q)", ["--nb-procs", "255"]),
 ]
 
 
