@@ -203,15 +203,19 @@ def sum_over_ranks(x: float, world: int) -> float:
     return float(t.item())
 
 
-# ---- CPU baseline (oracle, rank 0 at N=1 only) ------------------------------------
+# ---- CPU baseline (oracle, rank 0) -------------------------------------------------
 CPU_PROFILES = ("udp4", "tcp4")        # the headline stream, and every packet hashed
 CPU_VARIANTS = ("bit_serial", "table")  # toeplitz_hash as written; 12x256 byte tables
+CPU_RUNS = 3                            # timed windows per cell: median, min, max
 
 
 def cpu_worker(spec: str) -> int:
     """One pinned CPU-baseline process (bench.py --cpu-worker prof:variant:secs:cpu):
     the oracle's toeplitz_dispatch restatement over 2^20 packets of the stream,
-    one call per packet, repeated for about `secs` after a start line on stdin."""
+    one call per packet, repeated for about `secs` per timed window.  Every
+    "go" line on stdin starts one window; the answer carries the window's
+    CLOCK_MONOTONIC start and end, so the parent can check that the windows of
+    a cell's processes overlapped."""
     prof, variant, secs, cpu = spec.split(":")
     if cpu != "-":
         os.sched_setaffinity(0, {int(cpu)})     # what taskset -c does
@@ -225,67 +229,133 @@ def cpu_worker(spec: str) -> int:
     oracle.bench_dispatch(win, 64, lens, c, 1, fast)
     reps = max(1, int(float(secs) / max(time.perf_counter() - t0, 1e-6)))
     print("ready", flush=True)
-    sys.stdin.readline()
-    t0 = time.perf_counter()
-    oracle.bench_dispatch(win, 64, lens, c, reps, fast)
-    print(json.dumps({"pkts": reps * n, "secs": time.perf_counter() - t0}), flush=True)
+    while sys.stdin.readline().strip() == "go":
+        t0 = time.monotonic()
+        oracle.bench_dispatch(win, 64, lens, c, reps, fast)
+        t1 = time.monotonic()
+        print(json.dumps({"pkts": reps * n, "t0": t0, "t1": t1}), flush=True)
     return 0
 
 
-def _cpu_run(prof: str, variant: str, secs: float, cpus) -> float:
-    """Mpkt/s of len(cpus) pinned worker processes started together."""
+def _cpu_run(prof: str, variant: str, secs: float, cpus, runs: int = CPU_RUNS):
+    """len(cpus) pinned worker processes, started once and released together
+    for `runs` windows.  A window's rate is the sum of the processes' own rates;
+    `overlap` is the shortest common stretch of a window over its longest
+    process (1.0 = they ran side by side the whole time)."""
     import subprocess
+    import statistics
 
     procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--cpu-worker",
                                f"{prof}:{variant}:{secs}:{cpu}"],
                               stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
              for cpu in cpus]
+    rates, overlaps = [], []
     try:
         for p in procs:
             if p.stdout.readline().strip() != "ready":
                 raise RuntimeError("cpu worker failed to start")
+        for _ in range(runs):
+            for p in procs:
+                p.stdin.write("go\n")
+                p.stdin.flush()
+            res = [json.loads(p.stdout.readline()) for p in procs]
+            rates.append(sum(r["pkts"] / (r["t1"] - r["t0"]) for r in res) / 1e6)
+            common = min(r["t1"] for r in res) - max(r["t0"] for r in res)
+            overlaps.append(max(0.0, common) / max(r["t1"] - r["t0"] for r in res))
         for p in procs:
-            p.stdin.write("go\n")
+            p.stdin.write("end\n")
             p.stdin.flush()
-        res = [json.loads(p.stdout.readline()) for p in procs]
     finally:
         for p in procs:
             p.wait(timeout=600)
-    return sum(r["pkts"] for r in res) / max(r["secs"] for r in res) / 1e6
+    return {"mpps": round(statistics.median(rates), 2), "min": round(min(rates), 2),
+            "max": round(max(rates), 2), "runs": len(rates),
+            "overlap": round(min(overlaps), 3)}
+
+
+def cpu_quota():
+    """CPUs this job may keep busy: the cgroup CPU quota (v2 cpu.max, else v1
+    cfs_quota/period), capped by the affinity mask.  (count, source)."""
+    allowed = len(os.sched_getaffinity(0))
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = Path(path).read_text().split()[:2]
+            if q != "max":
+                n = max(1, -(-int(q) // int(per)))
+                return min(n, allowed), f"cgroup cpu.max {q} {per}"
+        except (OSError, ValueError):
+            pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        if q > 0:
+            return min(allowed, max(1, -(-q // per))), f"cgroup cfs_quota_us {q} / {per}"
+    except (OSError, ValueError):
+        pass
+    return allowed, "no cgroup CPU quota: sched_getaffinity"
+
+
+def physical_cores(cpus):
+    """One logical CPU per physical core (the first SMT sibling), in order."""
+    seen, out = set(), []
+    for c in cpus:
+        try:
+            sib = Path(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read_text()
+            key = min(_cpulist(sib))
+        except (OSError, ValueError):
+            key = c
+        if key not in seen:
+            seen.add(key)
+            out.append(c)
+    return out
 
 
 def cpu_baseline(args, nb_queues):
     """the reference's algorithm on the GPU box's host cores.
     Both ports (bit-serial as the reference writes toeplitz_hash, and
     table-driven), on the headline UDP stream and all-TCP, on 1 core (the
-    reference's single dispatching lcore, ff_dpdk_if.c:1653) and on every core
-    one GPU's share of the box (16), as independent
-    processes pinned one per core, and on every core the process may use
-    (sched_getaffinity: nproc on a dedicated box), SURVEY §8(d).  `value` is
-    the bit-serial port on 1 core over the bench's own stream (measured first,
-    then udp4 and tcp4)."""
-    cpus = sorted(os.sched_getaffinity(0))
-    share = cpus[: max(1, min(16, len(cpus)))]      # one GPU's share of the box's cores
-    cells = [cpus[:1], share]
+    reference's single dispatching lcore, ff_dpdk_if.c:1653) and on one GPU's
+    share of the box (16 cores), as independent processes pinned one per
+    physical core; and on every core the job's CPU quota lets it keep busy
+    (cgroup cpu.max, stated), SURVEY §8(d).  Every cell is the median of
+    CPU_RUNS timed windows with its min and max.  `value` is the bit-serial
+    port on 1 core over the bench's own stream."""
+    allowed = sorted(os.sched_getaffinity(0))
+    phys = physical_cores(allowed) or allowed
+    quota, qsrc = cpu_quota()
+    share_n = max(1, min(16, quota, len(phys)))
+    share = phys[:share_n]                          # one GPU's share of the box's cores
+    cells = [phys[:1], share]
     profs = list(dict.fromkeys([args.profile, *CPU_PROFILES]))   # the bench's own stream first
-    secs = max(0.5, args.cpu_seconds / (len(cells) * len(profs) * len(CPU_VARIANTS) + 1))
+    secs = max(0.3, args.cpu_seconds / ((len(cells) * len(profs) * len(CPU_VARIANTS) + 1) *
+                                        CPU_RUNS))
     by = {}
     for prof in profs:
         by[prof] = {}
         for var in CPU_VARIANTS:
             by[prof][var] = {}
             for cs in cells:
-                by[prof][var][str(len(cs))] = round(_cpu_run(prof, var, secs, cs), 2)
-                print(f"cpu_baseline {prof} {var} {len(cs)} cores: "
-                      f"{by[prof][var][str(len(cs))]} Mpkt/s", file=sys.stderr, flush=True)
-    # every core the process may use: the headline cell only (one pinned
-    # process per core; hundreds of interpreter start-ups per cell otherwise)
-    if len(cpus) > len(share):
-        by[args.profile]["bit_serial"][str(len(cpus))] = round(
-            _cpu_run(args.profile, "bit_serial", secs, cpus), 2)
-        print(f"cpu_baseline {args.profile} bit_serial {len(cpus)} cores: "
-              f"{by[args.profile]['bit_serial'][str(len(cpus))]} Mpkt/s", file=sys.stderr,
+                cell = _cpu_run(prof, var, secs, cs)
+                by[prof][var][str(len(cs))] = cell
+                print(f"cpu_baseline {prof} {var} {len(cs)} cores: {cell}", file=sys.stderr,
+                      flush=True)
+    # every core the quota lets the job keep busy: the headline cell only
+    all_cpus = (phys + [c for c in allowed if c not in set(phys)])[:quota]
+    if quota > share_n:
+        cell = _cpu_run(args.profile, "bit_serial", secs, all_cpus)
+        by[args.profile]["bit_serial"][str(quota)] = cell
+        print(f"cpu_baseline {args.profile} bit_serial {quota} cores: {cell}", file=sys.stderr,
               flush=True)
+        all_note = (f"{quota} pinned processes, the job's CPU quota ({qsrc}); physical cores "
+                    "first, then SMT siblings")
+    else:
+        all_note = (f"the job's CPU quota is {quota} CPUs ({qsrc}): every core it may keep "
+                    f"busy is the {share_n}-core cell itself")
+    all_cell = by[args.profile]["bit_serial"][str(max(quota, share_n))]
+    share_cell = by[args.profile]["bit_serial"][str(share_n)]
+    if all_cell["mpps"] < share_cell["mpps"]:
+        all_note += (f"; below the {share_n}-core cell: the extra processes share cores "
+                     "(SMT siblings or an over-committed quota)")
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -295,18 +365,20 @@ def cpu_baseline(args, nb_queues):
     except OSError:
         pass
     head = args.profile
+    one = by[head]["bit_serial"]["1"]
     return {
-        "value": by[head]["bit_serial"]["1"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
-        "sample": f"2^20 packets of each stream re-run for ~{secs:.1f}s per cell, one "
-                  "toeplitz_dispatch call per packet (oracle restatement, gcc -O2 fs/lib "
-                  f"flags), processes pinned one per core; host CPU: {cpu}",
-        "per_gpu_share": {"value": by[head]["bit_serial"][str(len(share))], "unit": "Mpkt/s",
-                          "cores": len(share),
+        "value": one["mpps"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
+        "min": one["min"], "max": one["max"], "runs": one["runs"],
+        "sample": f"2^20 packets of each stream re-run for ~{secs:.2f}s per timed window, "
+                  f"median of {CPU_RUNS} windows per cell, one toeplitz_dispatch call per "
+                  "packet (oracle restatement, gcc -O2 fs/lib flags), processes pinned one "
+                  f"per physical core; host CPU: {cpu}; {len(allowed)} CPUs in the affinity "
+                  f"mask, quota {quota} ({qsrc})",
+        "per_gpu_share": {"value": share_cell["mpps"], "min": share_cell["min"],
+                          "max": share_cell["max"], "unit": "Mpkt/s", "cores": share_n,
                           "note": "the 16 host cores one GPU of the box is given"},
-        "all_cores": {"value": by[head]["bit_serial"][str(len(cpus))], "unit": "Mpkt/s",
-                      "cores": len(cpus),
-                      "note": "every core this process may run on (sched_getaffinity), "
-                              "one pinned process per core"},
+        "all_cores": {"value": all_cell["mpps"], "min": all_cell["min"], "max": all_cell["max"],
+                      "unit": "Mpkt/s", "cores": max(quota, share_n), "note": all_note},
         "by_profile": by,
     }
 
@@ -341,7 +413,59 @@ def probe_traffic(batches, n, stride, steps, mode=0):
     return ev[0].elapsed_time(ev[1]) / steps / 1e3
 
 
-def pcie_inclusive(profile: str):
+def _cpulist(text: str):
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def gpu_placement(device: str):
+    """NUMA node of the GPU (PCI address from device_identity) and the CPU the
+    host-resident dispatcher thread is pinned to: the first CPU of that node
+    this process may run on (the reference's dispatching lcore sits beside its
+    NIC and GPU).  None where sysfs does not say."""
+    node, cpu = None, None
+    try:
+        node = int(Path(f"/sys/bus/pci/devices/{device}.0/numa_node").read_text())
+    except (OSError, ValueError):
+        node = None
+    allowed = sorted(os.sched_getaffinity(0))
+    if node is not None and node >= 0:
+        try:
+            local = _cpulist(Path(f"/sys/devices/system/node/node{node}/cpulist").read_text())
+            mine = [c for c in local if c in set(allowed)]
+            cpu = mine[0] if mine else None
+        except (OSError, ValueError):
+            cpu = None
+    return {"gpu_node": node, "dispatch_cpu": cpu}
+
+
+def _cbench_rows(lines, keys):
+    """One row per (api, burst) from YRSS_CBENCH_REPEAT runs: the median run's
+    fields, its spread, and every run's rate, host cycles and placement."""
+    groups = {}
+    for d in lines:
+        groups.setdefault((d["api"], d["burst"]), []).append(d)
+    rows = []
+    for (_, _), runs in groups.items():
+        runs_sorted = sorted(runs, key=lambda d: d["mpps"])
+        med = runs_sorted[len(runs_sorted) // 2]
+        row = {k: med.get(k) for k in keys if k in med}
+        row["mpps"] = med["mpps"]
+        row["mpps_min"] = runs_sorted[0]["mpps"]
+        row["mpps_max"] = runs_sorted[-1]["mpps"]
+        row["runs"] = [{k: d.get(k) for k in ("mpps", "poll_cycles", "submit_cycles",
+                                                "cpu_start", "cpu", "cpu_node", "pool_node")
+                        if k in d} for d in runs]
+        rows.append(row)
+    return rows
+
+
+def pcie_inclusive(profile: str, place=None):
     """Host-resident rates from tools/yrss_cbench (C host over the C ABI):
     DPDK-layout mbuf pool of 2^20 packets in host memory; bursts of 1024 (BASELINE's
     logical burst) and 32K with two in flight, and 1M; the persistent worker at
@@ -351,13 +475,15 @@ def pcie_inclusive(profile: str):
     exe = ROOT / "tools" / "yrss_cbench"
     if not exe.exists():
         return None
+    place = place or {}
+    pin = {} if place.get("dispatch_cpu") is None else {"YRSS_CBENCH_CPU": str(place["dispatch_cpu"])}
     out = []
     # (burst, bursts in flight over that many contexts with YRSS_F_ASYNC)
     for burst, inflight in ((1024, 2), (32768, 2), (1 << 20, 1)):
         try:
             r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
-                               env={**os.environ, "YRSS_CBENCH_MODES": "013",
+                               env={**os.environ, **pin, "YRSS_CBENCH_MODES": "013",
                                     "YRSS_CBENCH_INFLIGHT": str(inflight)})
         except subprocess.TimeoutExpired:
             return None
@@ -371,37 +497,42 @@ def pcie_inclusive(profile: str):
     # persistent worker, mbuf pointers, (data, data_len) pairs and windows the
     # dispatcher copies into a registered ring ("2"), one output set per ring
     # slot: 32-packet bursts on 128 workgroups, 1024-packet bursts on 32 (the
-    # best counts of the sweeps), ring depth 4 x workgroups
+    # best counts of the sweeps), ring depth 4 x workgroups.
+    # Three runs each (median, spread), every run with its host cycles per
+    # burst and the thread's and pool's NUMA placement beside the GPU's.
     for frames, burst, blocks in (("0", 32, 128), ("0", 1024, 32), ("1", 32, 128),
                                   ("1", 1024, 32), ("2", 32, 128), ("2", 1024, 32)):
         try:
             r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
-                               env={**os.environ, "YRSS_CBENCH_MODES": "4",
+                               env={**os.environ, **pin, "YRSS_CBENCH_MODES": "4",
+                                    "YRSS_CBENCH_REPEAT": "3",
                                     "YRSS_CBENCH_WORKER_DEPTH": str(4 * blocks),
                                     "YRSS_CBENCH_WORKER_BLOCKS": str(blocks),
                                     "YRSS_CBENCH_WORKER_SLOTOUT": "1",
                                     "YRSS_CBENCH_WORKER_FRAMES": frames})
         except subprocess.TimeoutExpired:
             break
+        lines = []
         for line in r.stdout.splitlines():
             try:
-                d = json.loads(line)
+                lines.append(json.loads(line))
             except ValueError:
                 continue
-            # bytes crossing PCIe per packet, GPU reads: mbuf pointer 8 +
-            # header 64 + window 64 (64-byte packets), or pointer 8 + len 2 +
-            # window 64, or len 2 + window 64; writes q 2 + hash 4 + qidx 4
-            rd = {"0": 136, "1": 74, "2": 66}[frames]
-            gbs = d["mpps"] * 1e6 * (rd + 10) / 1e9
-            out.append({"api": d["api"], "burst": d["burst"], "inflight": d.get("inflight", 1),
-                        "blocks": d.get("blocks"), "mpps": d["mpps"], "note": d.get("note", ""),
-                        "link_bytes_per_pkt": rd + 10, "link_GBps": round(gbs, 2),
-                        "link_frac": round(gbs / PCIE_GEN5_X16_GBS, 4)})
+        # bytes crossing PCIe per packet, GPU reads: mbuf pointer 8 +
+        # header 64 + window 64 (64-byte packets), or pointer 8 + len 2 +
+        # window 64, or len 2 + window 64; writes q 2 + hash 4 + qidx 4
+        rd = {"0": 136, "1": 74, "2": 66}[frames]
+        for row in _cbench_rows(lines, ("api", "burst", "inflight", "blocks", "note")):
+            gbs = row["mpps"] * 1e6 * (rd + 10) / 1e9
+            row.update({"link_bytes_per_pkt": rd + 10, "link_GBps": round(gbs, 2),
+                        "link_frac": round(gbs / PCIE_GEN5_X16_GBS, 4),
+                        "gpu_node": place.get("gpu_node")})
+            out.append(row)
     return out or None
 
 
-def pcie_fanout(profile: str, world: int):
+def pcie_fanout(profile: str, world: int, place=None):
     """Host-resident rate of ONE dispatcher thread fanning its bursts out over
     all `world` GPUs (yrss_fanout_*, tools/yrss_cbench mode 5): the reference's
     single dispatching lcore (ff_dpdk_if.c:1653) with N PCIe links behind it.
@@ -411,6 +542,8 @@ def pcie_fanout(profile: str, world: int):
     exe = ROOT / "tools" / "yrss_cbench"
     if not exe.exists():
         return None
+    place = place or {}
+    pin = {} if place.get("dispatch_cpu") is None else {"YRSS_CBENCH_CPU": str(place["dispatch_cpu"])}
     out = []
     one = bool(os.environ.get("YRSS_BENCH_ONE_DEVICE"))   # rehearsal: N contexts, device 0
     devs = ",".join("0" if one else str(d) for d in range(world))
@@ -418,20 +551,23 @@ def pcie_fanout(profile: str, world: int):
         try:
             r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
-                               env={**os.environ, "YRSS_CBENCH_MODES": "5",
+                               env={**os.environ, **pin, "YRSS_CBENCH_MODES": "5",
+                                    "YRSS_CBENCH_REPEAT": "3",
                                     "YRSS_CBENCH_FANOUT_DEVICES": devs,
                                     "YRSS_CBENCH_WORKER_DEPTH": str(4 * blocks),
                                     "YRSS_CBENCH_WORKER_BLOCKS": str(blocks),
                                     "YRSS_CBENCH_WORKER_FRAMES": frames})
         except subprocess.TimeoutExpired:
             break
+        lines = []
         for line in r.stdout.splitlines():
             try:
-                d = json.loads(line)
+                lines.append(json.loads(line))
             except ValueError:
                 continue
-            out.append({"api": d["api"], "burst": d["burst"], "gpus": d["gpus"],
-                        "inflight": d["inflight"], "blocks": d["blocks"], "mpps": d["mpps"]})
+        for row in _cbench_rows(lines, ("api", "burst", "gpus", "inflight", "blocks")):
+            row["gpu_node"] = place.get("gpu_node")
+            out.append(row)
     return out or None
 
 
@@ -657,9 +793,10 @@ def main(argv=None):
         barrier(world)                    # every rank's device work is done
         if rank == 0:
             eng.close()                   # release the device buffers first
+            place = gpu_placement(devices[0])
             if world == 1:
-                pcie = pcie_inclusive(args.profile)
-            fan = pcie_fanout(args.profile, world)
+                pcie = pcie_inclusive(args.profile, place)
+            fan = pcie_fanout(args.profile, world, place)
         barrier(world)
 
     if rank == 0:

@@ -535,11 +535,15 @@ struct yrss_fault {
     uint32_t value;
 };
 
-/* Synchronises the device and reports (then clears) the fault record: 0 = no
- * guard fired since the last call, -EIO = one did (the record is printed to
- * stderr).  The host-synchronous entry points check it themselves and return
- * -EIO, as does yrss_worker_poll.  The reference has no equivalent: its
- * per-packet rte_ring_enqueue cannot fail this way (ff_dpdk_if.c:1087-1093). */
+/* Synchronises the context's own streams (its internal one and the stream of
+ * its last device batch, not the whole device) and reports (then clears) the
+ * fault record: 0 = no guard fired since the last call, -EIO = one did (the
+ * record is printed to stderr).  The host-synchronous entry points check it
+ * themselves and return -EIO.  A persistent-worker burst carries its own
+ * record: yrss_worker_poll returns -EIO for exactly the burst whose guard
+ * fired (other bursts in flight are unaffected) and copies the record here
+ * when this one is empty.  The reference has no equivalent: its per-packet
+ * rte_ring_enqueue cannot fail this way (ff_dpdk_if.c:1087-1093). */
 int yrss_status(yrss_ctx *ctx);
 /* Same, copying the record (code 0 = none) instead of printing it. */
 int yrss_fault_info(yrss_ctx *ctx, struct yrss_fault *out);

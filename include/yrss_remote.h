@@ -22,7 +22,12 @@
  * ring (their windows are still in the slots), so no burst is lost.  A helper
  * that stops making progress (a hung GPU) makes the poll return -ETIMEDOUT
  * after the context's timeout; yrss_remote_restart then kills and replaces it.
- * The helper dies with its lcore (PR_SET_PDEATHSIG).
+ * The helper dies with its lcore: PR_SET_PDEATHSIG, which fires when the
+ * spawning THREAD exits, so call yrss_remote_start and yrss_remote_restart
+ * from the long-lived lcore thread, not from a short-lived init or control
+ * thread; the helper also leaves once its parent process is gone (it polls
+ * getppid() while idle).  A restarted helper re-runs only the tickets not yet
+ * completed: a completed ticket's outputs and status never change.
  *
  * Results are bit-identical to yrss_worker_submit_frames (toeplitz_dispatch,
  * ff_dpdk_if.c:1945-2113, and the process_packets FIFO lists, :1058-1094).

@@ -123,3 +123,23 @@ def test_remote_library_exports_its_header_and_no_hip():
     deps = subprocess.run(["ldd", str(remote.LIB_PATH)], capture_output=True, text=True).stdout
     assert "amdhip" not in deps and "hsa" not in deps
     assert remote.HELPER_PATH.exists() and os.access(remote.HELPER_PATH, os.X_OK)
+
+
+def test_registration_shim_notes_its_cost_once():
+    """yrss_toeplitz_dispatch prints its per-call cost and the burst hook it
+    should be replaced by, once per process (no context: no GPU call)."""
+    code = (
+        "import ctypes\n"
+        "from yastack_amd import abi\n"
+        "lib = abi.load()\n"
+        "f = lib.yrss_toeplitz_dispatch\n"
+        "f.restype = ctypes.c_int\n"
+        "f.argtypes = [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16]\n"
+        "buf = ctypes.create_string_buffer(64)\n"
+        "print([f(buf, 64, 0, 3) for _ in range(3)])\n")
+    r = subprocess.run([os.environ.get("PYTHON", "python"), "-c", code], capture_output=True,
+                       text=True, cwd=str(abi.LIB_PATH.parents[2]), timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "[-1, -1, -1]"
+    assert r.stderr.count("serves ONE packet per GPU round trip") == 1, r.stderr
+    assert "yrss_dispatch_burst" in r.stderr and "118.6 ns" in r.stderr

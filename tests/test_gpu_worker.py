@@ -488,3 +488,41 @@ def test_device_batch_beside_other_process_worker(dev):
             if p.poll() is None:
                 p.kill()
         assert shared < solo + 5.0, (solo, shared)
+
+
+def test_worker_guard_fault_is_per_burst(dev, oracle_mod, monkeypatch):
+    """A list guard that fires in one worker burst fails that burst alone
+    (-EIO), with several bursts of other workgroups in flight at once; the
+    record names it and the bursts around it stay bit-exact (ADVICE r03:
+    the context-wide record used to be taken by whichever poll came first)."""
+    import errno
+
+    monkeypatch.setenv("YRSS_WORKER_INJECT", "5")   # test hook: ticket 5 fires a guard
+    cfg = (8, 8, 1, 0)
+    nb, per = 12, 40
+    frames = _frames(oracle_mod, nb * per, 77)
+    pool, ptrs, _ = _fake_mbufs(frames)
+    q_all, h_all, _, _ = _expect(oracle_mod, frames, cfg)
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        eng.register_host_memory(pool.ctypes.data, pool.nbytes)
+        eng.worker_start(16, 4)
+        tickets = [eng.worker_submit(ptrs[i * per:(i + 1) * per]) for i in range(nb)]
+        for i, t in enumerate(tickets):
+            q = q_all[i * per:(i + 1) * per]
+            if t == 5:
+                with pytest.raises(abi.YrssError) as ei:
+                    eng.worker_poll(t)
+                assert ei.value.errno == errno.EIO
+                continue
+            r = eng.worker_poll(t)
+            qi, qs = oracle_mod.process_burst(q, cfg[1])
+            _check(r, q, h_all[i * per:(i + 1) * per], qi, qs)
+        code, kernel, where, value = eng.fault_info()
+        assert (code, kernel, where, value) == (abi.FAULT_LIST_RANGE, abi.K_WORKER, 5, 0xdead)
+        assert eng.fault_info()[0] == abi.FAULT_NONE
+        # later bursts are unaffected
+        t = eng.worker_submit(ptrs[:per])
+        qi, qs = oracle_mod.process_burst(q_all[:per], cfg[1])
+        _check(eng.worker_poll(t), q_all[:per], h_all[:per], qi, qs)
+        eng.worker_stop()
+        eng.unregister_host_memory(pool.ctypes.data)

@@ -40,10 +40,13 @@ def main() -> int:
         e = SoftRss(npr, npr, 1, 1, device=0, max_burst=0, lib_path=str(ROOT / args.lib))
         w, l = e.synth(abi.SYN_TCP4, n, 0)
         out = e.alloc_out(n, w.device)
-        for _ in range(5):
+        buf = np.zeros(2048 * 8 * 8, np.uint64)
+        for _ in range(4):
             e.dispatch_dev(w, l, 64, n, out=out)
         torch.cuda.synchronize()
-        buf = np.zeros(2048 * 8 * 8, np.uint64)
+        assert lib.yrss_debug_line_prof(buf.ctypes.data, buf.nbytes) > 0   # read + clear
+        e.dispatch_dev(w, l, 64, n, out=out)
+        torch.cuda.synchronize()
         assert lib.yrss_debug_line_prof(buf.ctypes.data, buf.nbytes) > 0
         p = buf.reshape(2048, 8, 8).astype(np.int64)
         used = p[:, :, 0] != 0
@@ -69,6 +72,25 @@ def main() -> int:
               f"end {(ends.min() - t0) * 10:.0f}-{(ends.max() - t0) * 10:.0f} ns after the first start")
         per_span = (p[:, :, len(PH)] - p[:, :, 0])[used] * 10
         print(f"   span total mean {per_span.mean():.0f} ns")
+        # slots 7 / 6 of span 0: kernel entry and the look-back's end
+        entry = p[:, 0, 7][used[:, 0]]
+        lbend = p[:, 0, 6][used[:, 0]]
+        if (entry > 0).all() and (lbend > 0).all():
+            k0 = entry.min()
+            pro = (lbend - entry) * 10
+            print(f"   entry spread {(entry.max() - k0) * 10:.0f} ns; entry -> look-back done mean "
+                  f"{pro.mean():.0f} p90 {np.percentile(pro, 90):.0f} ns; look-back -> first span "
+                  f"{((first - lbend) * 10).mean():.0f} ns")
+            endk = (ends - k0) * 10
+            ids = np.nonzero(used[:, 0])[0]
+            print(f"   end after first entry: p10 {np.percentile(endk, 10):.0f} p50 "
+                  f"{np.percentile(endk, 50):.0f} p90 {np.percentile(endk, 90):.0f} max "
+                  f"{endk.max():.0f} ns")
+            xcd = " ".join(f"{endk[ids % 8 == x].mean() / 1e3:.1f}" for x in range(8))
+            print(f"   mean end by blockIdx % 8 (XCD), us: {xcd}")
+            half = len(ids) // 2
+            print(f"   mean end, first / second half of the grid: "
+                  f"{endk[ids < half].mean() / 1e3:.1f} / {endk[ids >= half].mean() / 1e3:.1f} us")
         e.close()
     return 0
 

@@ -4,7 +4,7 @@ counts x streams x ragged sizes, q / hash / qidx / qstart compared in full and
 the fault record asserted empty after every batch.  Prints one line per case
 and exits non-zero on the first mismatch.
 
-    python tools/quick_parity.py [--big]
+    python tools/quick_parity.py [--big] [--lib ab/lib/libyrss_X.so] [--tune k=v;...]
 """
 from __future__ import annotations
 
@@ -24,13 +24,22 @@ def main() -> int:
     from yastack_amd import SoftRss, abi
 
     big = "--big" in sys.argv
+    lib = None
+    tune = {}
+    for i, a in enumerate(sys.argv):
+        if a == "--lib":
+            lib = str(ROOT / sys.argv[i + 1])
+        if a == "--tune":
+            tune = {k: int(v) for k, v in (kv.split("=") for kv in sys.argv[i + 1].split(";") if kv)}
     cfgs = [(3, 3, 1, 1), (2, 2, 1, 0), (8, 8, 1, 0), (8, 8, 1, 1), (16, 16, 1, 0),
             (64, 64, 1, 1), (255, 255, 1, 0), (4096, 256, 1, 1), (5, 3, 1, 0)]
     sizes = [4097, 5000, 300001] + ([1 << 22] if big else [])
     profs = [abi.SYN_TCP4, abi.SYN_FUZZ, abi.SYN_UDP4, abi.SYN_IMIX]
     bad = 0
     for cfg in cfgs:
-        with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        with SoftRss(*cfg, device=0, max_burst=0, lib_path=lib) as eng:
+            if tune:
+                eng.set_tuning(**tune)
             for prof in profs:
                 for n in sizes:
                     win, lens = eng.synth(prof, n, 1234 + n, stride=64)

@@ -14,12 +14,16 @@
  * 0-3 the one-call burst APIs, 4 the persistent worker, 5 the multi-GPU
  * fan-out (YRSS_CBENCH_FANOUT_DEVICES).
  */
+#define _GNU_SOURCE
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
 #include <time.h>
+#include <unistd.h>
 #include <x86intrin.h>
 
 #include "yrss.h"
@@ -43,6 +47,41 @@ static void fill_frames(void *const *m, uint32_t n, const uint8_t **data, uint16
         memcpy(&len[i], mb + YRSS_MBUF_OFF_DATA_LEN, 2);
         data[i] = buf + doff;
     }
+}
+
+/* Placement of the dispatcher thread and of the pool, carried in every JSON
+ * line so an outlier explains itself: the CPU the thread runs on (start of the
+ * run and at its report), that CPU's NUMA node, the node holding the pool's
+ * first and last page.  YRSS_CBENCH_CPU pins the thread before the pool is
+ * touched (first touch then places the pool on that CPU's node). */
+static int cpu_node(int cpu)
+{
+    char path[96];
+    for (int nd = 0; nd < 64; ++nd) {
+        snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/node%d", cpu, nd);
+        if (access(path, F_OK) == 0)
+            return nd;
+    }
+    return -1;
+}
+
+static int page_node(const void *addr)
+{
+    int node = -1;
+    /* get_mempolicy(&node, NULL, 0, addr, MPOL_F_NODE | MPOL_F_ADDR) */
+    if (syscall(SYS_get_mempolicy, &node, NULL, 0UL, addr, 3UL) != 0)
+        return -1;
+    return node;
+}
+
+static int g_cpu_start = -1;
+static int g_pool_node[2] = {-1, -1};
+
+static void print_placement(void)
+{
+    const int cpu = sched_getcpu();
+    printf(", \"cpu_start\": %d, \"cpu\": %d, \"cpu_node\": %d, \"pool_node\": [%d, %d]",
+           g_cpu_start, cpu, cpu_node(cpu), g_pool_node[0], g_pool_node[1]);
 }
 
 static double now(void)
@@ -166,7 +205,7 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
            "\"seconds\": %.3f, \"mpps\": %.2f, \"us_per_burst\": %.2f, \"thp\": %d, "
            "\"poll_cycles\": %.0f, \"submit_cycles\": %.0f, "
            "\"mode\": 4, \"note\": \"persistent kernel polls a ring of bursts in pinned "
-           "memory; %s read over PCIe\"}\n",
+           "memory; %s read over PCIe\"",
            frames == 2 ? "yrss_worker_submit_windows"
            : frames    ? "yrss_worker_submit_frames" : "yrss_worker_submit", profile, B, depth,
            blocks, (unsigned long long)pkts, t1 - t0, pkts / (t1 - t0) / 1e6,
@@ -174,6 +213,8 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
            nb ? (double)cyc_sub / nb : 0.0,
            frames == 2 ? "contiguous windows the dispatcher copied (one stretch per burst)"
            : frames    ? "windows of (data, data_len) pairs" : "mbuf headers + windows");
+    print_placement();
+    printf("}\n");
     fflush(stdout);
     free(tk);
     yrss_fini(ctx);
@@ -269,10 +310,12 @@ static int run_fanout(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
            "\"burst\": %u, \"gpus\": %u, \"inflight\": %llu, \"blocks\": %u, \"pkts\": %llu, "
            "\"seconds\": %.3f, \"mpps\": %.2f, \"mode\": 5, \"note\": \"one dispatcher "
            "thread, bursts round-robin over %u contexts' persistent workers, handed off in "
-           "submission order; %s read over PCIe\"}\n",
+           "submission order; %s read over PCIe\"",
            frames ? "yrss_fanout_submit_frames" : "yrss_fanout_submit", profile, B, nd,
            (unsigned long long)inflight, blocks, (unsigned long long)pkts, t1 - t0,
            pkts / (t1 - t0) / 1e6, nd, frames ? "windows" : "mbuf headers + windows");
+    print_placement();
+    printf("}\n");
     fflush(stdout);
     free(qs);
     yrss_fanout_fini(f);
@@ -344,6 +387,15 @@ int main(int argc, char **argv)
     const uint32_t pool = argc > 2 ? (uint32_t)atoi(argv[2]) : (1u << 20);
     const uint32_t burst_arg = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
     const double secs = argc > 4 ? atof(argv[4]) : 2.0;
+    const char *cpu_env = getenv("YRSS_CBENCH_CPU");
+    if (cpu_env && *cpu_env) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(atoi(cpu_env), &set);
+        if (sched_setaffinity(0, sizeof(set), &set) != 0)
+            perror("sched_setaffinity");
+    }
+    g_cpu_start = sched_getcpu();
 
     /* DPDK mbuf pools live in hugepage memzones; ask for transparent huge pages
      * (YRSS_CBENCH_THP=0 keeps 4 KiB pages) so IOMMU translation for the
@@ -376,6 +428,7 @@ int main(int argc, char **argv)
         return 1;
     }
     struct yrss_synth_params sp = {0x9E3779B97F4A7C15ull, profile, 1u << 20};
+    mem[0] = 0;                              /* first touch by this thread */
     for (uint32_t i = 0; i < pool; ++i) {
         uint8_t *m = mem + (size_t)i * MBUF_STRIDE;
         uint8_t *buf = m + MBUF_HDR;
@@ -395,6 +448,8 @@ int main(int argc, char **argv)
         mbufs[i] = m;
     }
 
+    g_pool_node[0] = page_node(mem);
+    g_pool_node[1] = page_node(mem + mem_sz - 1);
     struct yrss_config cfg;
     yrss_config_default(&cfg);
     const uint32_t bursts[] = {32, 1024, 32768, 1u << 20};
@@ -501,23 +556,31 @@ int main(int argc, char **argv)
         if (burst_arg)
             break;
     }
+    /* YRSS_CBENCH_REPEAT=k: the worker and fan-out runs k times each over the
+     * same pool (one JSON line per run: the spread of a placement) */
+    const char *rep_env = getenv("YRSS_CBENCH_REPEAT");
+    const int reps = rep_env && atoi(rep_env) > 0 ? atoi(rep_env) : 1;
     if (mode_env && strchr(mode_env, '4'))
         for (unsigned bi = 0; bi < 2; ++bi) {
             const uint32_t B = burst_arg ? burst_arg : bursts[bi];
-            const int rc = run_worker(&cfg, mem, mem_sz, arena, arena_sz, mbufs, pool, B, secs,
-                                      q_all, h_all, qi_all, profile, thp, fdata, flen);
-            if (rc)
-                return rc;
+            for (int r = 0; r < reps; ++r) {
+                const int rc = run_worker(&cfg, mem, mem_sz, arena, arena_sz, mbufs, pool, B, secs,
+                                          q_all, h_all, qi_all, profile, thp, fdata, flen);
+                if (rc)
+                    return rc;
+            }
             if (burst_arg)
                 break;
         }
     if (mode_env && strchr(mode_env, '5'))
         for (unsigned bi = 0; bi < 2; ++bi) {
             const uint32_t B = burst_arg ? burst_arg : bursts[bi];
-            const int rc = run_fanout(&cfg, mem, mem_sz, arena, arena_sz, mbufs, pool, B, secs,
-                                      q_all, h_all, qi_all, profile, fdata, flen);
-            if (rc)
-                return rc;
+            for (int r = 0; r < reps; ++r) {
+                const int rc = run_fanout(&cfg, mem, mem_sz, arena, arena_sz, mbufs, pool, B, secs,
+                                          q_all, h_all, qi_all, profile, fdata, flen);
+                if (rc)
+                    return rc;
+            }
             if (burst_arg)
                 break;
         }

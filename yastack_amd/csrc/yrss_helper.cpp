@@ -52,8 +52,13 @@ int main(int argc, char **argv)
         fprintf(stderr, "usage: yrss_helper --ring-fd FD (started by yrss_remote_start)\n");
         return 2;
     }
-    prctl(PR_SET_PDEATHSIG, SIGKILL);   // never outlive the lcore
-    if (getppid() == 1)
+    // Never outlive the lcore.  PR_SET_PDEATHSIG fires when the THREAD that
+    // spawned this process exits, which is the lcore process only if that
+    // thread is the long-lived lcore thread (yrss_remote.h); the loop below
+    // also leaves when the parent process itself is gone (getppid changes).
+    prctl(PR_SET_PDEATHSIG, SIGKILL);
+    const pid_t parent = getppid();
+    if (parent == 1)
         return 3;
     struct stat st;
     if (fstat(fd, &st) != 0 || (size_t)st.st_size < kHeaderBytes)
@@ -112,6 +117,14 @@ int main(int argc, char **argv)
             const uint32_t si = (uint32_t)(next % nslots);
             if (__atomic_load_n(&slots[si].seq, __ATOMIC_ACQUIRE) != next)
                 break;
+            if (__atomic_load_n(&done[si].ticket, __ATOMIC_ACQUIRE) == next) {
+                // completed by the helper this one replaced (a failed submit
+                // is published out of order): not re-run, so a client reading
+                // its outputs or status never sees them change
+                ++next;
+                busy = true;
+                continue;
+            }
             const uint32_t n = slots[si].n;
             uint8_t *d = data(si);
             uint64_t wt = 0;
@@ -146,6 +159,8 @@ int main(int argc, char **argv)
             idle = 0;     // bursts on the GPU: keep polling
         } else if (++idle > 4096) {
             usleep(20);   // nothing published for a while: yield the core
+            if (getppid() != parent)
+                break;    // the lcore process is gone
         }
     }
     yrss_worker_stop(ctx);

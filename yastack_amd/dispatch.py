@@ -18,6 +18,7 @@ parse/hash/compaction runs in the HIP kernels of libyrss.so.
 from __future__ import annotations
 
 import ctypes
+import errno
 from dataclasses import dataclass
 
 import numpy as np
@@ -126,12 +127,20 @@ class SoftRss:
     def close(self) -> None:
         if getattr(self, "_ctx", None) and self._ctx.value:
             # a device guard that fired and was never read (yrss_status /
-            # fault_info) is logged before the context goes (abi.FAULT_LOG)
+            # fault_info) is logged before the context goes (abi.FAULT_LOG);
+            # a context that already timed out on the GPU is not waited for
+            # again (yrss_fault_info drains the context's streams)
             f = abi.Fault()
-            if self._lib.yrss_fault_info(self._ctx, ctypes.byref(f)) == 0 and f.code:
+            if not getattr(self, "_hung", False) and \
+                    self._lib.yrss_fault_info(self._ctx, ctypes.byref(f)) == 0 and f.code:
                 abi.FAULT_LOG.append((int(f.code), int(f.kernel), int(f.where), int(f.value)))
             self._lib.yrss_fini(self._ctx)
             self._ctx = ctypes.c_void_p()
+
+    def _ck(self, rc: int, what: str) -> None:
+        if rc == -errno.ETIMEDOUT:
+            self._hung = True     # close() does not wait on this context again
+        abi.check(rc, what)
 
     def __enter__(self):
         return self
@@ -248,7 +257,7 @@ class SoftRss:
         """Complete the burst queued with ``async_=True`` (``yrss_wait``)."""
         rc = self._lib.yrss_wait(self._ctx)
         self._inflight = None
-        abi.check(rc, "yrss_wait")
+        self._ck(rc, "yrss_wait")
 
     # -- persistent burst worker ------------------------------------------------
     def worker_start(self, nslots: int = 16, nblocks: int = 4) -> None:
@@ -330,7 +339,7 @@ class SoftRss:
         if rc == -11:   # -EAGAIN
             return None
         res = self._wk.pop(ticket, None)
-        abi.check(rc, "yrss_worker_poll")
+        self._ck(rc, "yrss_worker_poll")
         return res
 
     def worker_stop(self) -> None:
