@@ -75,12 +75,13 @@ def main() -> int:
         # slots 7 / 6 of span 0: kernel entry and the look-back's end
         entry = p[:, 0, 7][used[:, 0]]
         lbend = p[:, 0, 6][used[:, 0]]
-        if (entry > 0).all() and (lbend > 0).all():
+        if (entry > 0).all():
             k0 = entry.min()
-            pro = (lbend - entry) * 10
-            print(f"   entry spread {(entry.max() - k0) * 10:.0f} ns; entry -> look-back done mean "
-                  f"{pro.mean():.0f} p90 {np.percentile(pro, 90):.0f} ns; look-back -> first span "
-                  f"{((first - lbend) * 10).mean():.0f} ns")
+            pro = (first - entry) * 10
+            print(f"   entry spread {(entry.max() - k0) * 10:.0f} ns; entry -> first span mean "
+                  f"{pro.mean():.0f} p90 {np.percentile(pro, 90):.0f} ns")
+            if (lbend > 0).all():
+                print(f"   entry -> look-back done mean {((lbend - entry) * 10).mean():.0f} ns")
             endk = (ends - k0) * 10
             ids = np.nonzero(used[:, 0])[0]
             print(f"   end after first entry: p10 {np.percentile(endk, 10):.0f} p50 "

@@ -76,8 +76,7 @@ struct ParseParams {
     const uint16_t *len;
     int16_t *q;
     uint32_t *hash;       // may be null
-    uint32_t *seg_cnt;    // [ncol][nb] per-chunk counts, chunk-major (a chunk's nb
-                          // counts contiguous), or null
+    uint32_t *seg_cnt;    // [nb][ncol] per-chunk counts, bucket-major, or null
     uint16_t *rank;       // kCount == 2: packet's rank among its chunk's same-bucket packets
     uint32_t *fault;      // host-coherent fault record (report_fault), or null
     uint32_t n;
@@ -96,14 +95,6 @@ struct ParseParams {
     uint32_t kni_enable;
     uint32_t out16;       // full output bursts as 16-byte write-through stores (0: lane-granular)
     uint32_t rank_pack;   // kCount == 2: the rank word is bucket << (ct_shift + 6) | rank
-    // kCount: the batch's per-bucket counts of each of 8 regions of chunk
-    // columns (8 x nb words; region x = columns [reg_col[x], reg_col[x + 1]),
-    // the columns of the line scatter's workgroups on one XCD): each
-    // workgroup adds its own (one atomic per region and bucket); workgroup 0
-    // zeroes the other parity's regions for the next batch
-    uint32_t *tot_add;
-    uint32_t *tot_zero;
-    uint32_t reg_col[8];
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
@@ -584,9 +575,6 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     if (kCount)
         for (uint32_t e = lane; e < kCntWords; e += kWave)
             cnt_w[e] = 0;
-    if (kCount && P.tot_zero && blockIdx.x == 0)
-        for (uint32_t e = threadIdx.x; e < 8u * P.nb; e += kBlock)
-            P.tot_zero[e] = 0u;
     __syncthreads();
 
     // Chunks are dealt round-robin (chunk c to wave c mod W), so at any moment
@@ -664,50 +652,22 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
     if (kCount) {
         // Workgroup flush: for its j-th chunk each of the 8 waves owns column
         // blockIdx.x * 8 + w + j * W, so the workgroup's columns of round j
-        // are 8 consecutive chunks, i.e. (chunk-major matrix) 8 nb contiguous
-        // words.  Thread e takes bucket e % nb, wave (e / nb) % 8, round
-        // e / (8 nb): every store is whole lines (a store costs the lines its
-        // lanes touch; the per-wave flush of round 2 cost 2 us on UDP and 33
-        // us at 256 buckets, profiles/r02_v30_cntwg_ab.log, and the
-        // bucket-major matrix of round 3 left 32-byte pieces of lines).
-        // The workgroup's counts per region and bucket (its chunks, all
-        // waves) are summed in the staging tiles (dead here) on the way and
-        // added to the batch's region totals with one atomic each: the line
-        // scatter reads them instead of waiting for a scan of the matrix.
-        __syncthreads();
-        uint32_t *wsum = reinterpret_cast<uint32_t *>(smem + kTblBytes);
-        const bool tot = P.tot_add != nullptr && 8u * P.nb <= (uint32_t)(kWaves * kStageBytes / 4);
-        if (tot)
-            for (uint32_t e = threadIdx.x; e < 8u * P.nb; e += kBlock)
-                wsum[e] = 0u;
+        // are 8 consecutive words of every bucket row.  Thread e takes wave
+        // e % 8, bucket (e / 8) % nb, round e / (8 nb): a 64-lane store then
+        // covers 8 rows x 32 contiguous bytes instead of one word in each of
+        // 64 rows (a store costs the lines its lanes touch; the per-wave flush
+        // it replaced cost 2 us on UDP and 33 us at 256 buckets,
+        // profiles/r02_v30_cntwg_ab.log).
         __syncthreads();
         const uint32_t g0 = blockIdx.x * kWaves;
         const uint32_t kmax = P.nchunk > g0 ? (P.nchunk - g0 + W - 1) / W : 0u;
         const uint32_t per_round = kWaves * P.nb;
         for (uint32_t e = threadIdx.x; e < kmax * per_round; e += kBlock) {
             const uint32_t j = e / per_round, r = e - j * per_round;
-            const uint32_t w = r / P.nb, b = r - w * P.nb;
+            const uint32_t b = r / kWaves, w = r - b * kWaves;
             const uint32_t col = g0 + w + j * W;
-            if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords) {
-                const uint32_t v = cnt_base[w * kCntWords + j * P.nb + b];
-                P.seg_cnt[(size_t)col * P.nb + b] = v;
-                if (tot && v) {
-                    uint32_t x = 0;
-#pragma unroll
-                    for (uint32_t i = 1; i < 8u; ++i)
-                        x += col >= P.reg_col[i] ? 1u : 0u;
-                    atomicAdd(&wsum[x * P.nb + b], v);
-                }
-            }
-        }
-        if (tot) {
-            __syncthreads();
-            for (uint32_t e = threadIdx.x; e < 8u * P.nb; e += kBlock) {
-                const uint32_t v = wsum[e];
-                if (v)
-                    __hip_atomic_fetch_add(P.tot_add + e, v, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords)
+                P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
         }
     }
 }
@@ -744,40 +704,13 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
     return x;
 }
 
-// Inclusive scan inside aligned groups of `seg` lanes (a power of two <= 64):
-// DPP row shifts with the group boundary masked (rows of 16 lanes bound them
-// anyway), then row 0's / rows 0-1's last lane into the next row(s) when a
-// group spans rows
-__device__ __forceinline__ uint32_t seg_incl_scan(uint32_t x, uint32_t lane, uint32_t seg)
-{
-    const uint32_t li = lane & (seg - 1u);
-    uint32_t y;
-    y = __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);   // row_shr:1
-    x += li >= 1u ? y : 0u;
-    y = __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);   // row_shr:2
-    x += li >= 2u ? y : 0u;
-    y = __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);   // row_shr:4
-    x += li >= 4u ? y : 0u;
-    y = __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);   // row_shr:8
-    x += li >= 8u ? y : 0u;
-    if (seg >= 32u) {
-        y = __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
-        x += y;
-    }
-    if (seg >= 64u) {
-        y = __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
-        x += y;
-    }
-    return x;
-}
-
 struct ScanParams {
-    const uint32_t *cnt;     // [ncol][nb] (chunk-major, the parse kernel's)
+    const uint32_t *cnt;     // [nb][ncol]
     uint32_t *off;           // [nb][ncol] exclusive prefix per chunk column
     uint32_t *totals;        // [nb]
     unsigned long long *status;   // [nb][tiles]: flag | epoch:31 | value:32
     uint32_t *fault;
-    uint32_t nchunk, ncol, tiles, epoch, nb;
+    uint32_t nchunk, ncol, tiles, epoch;
 };
 
 __device__ __forceinline__ unsigned long long scan_status(uint32_t epoch, bool incl, uint32_t v)
@@ -792,13 +725,8 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
     const uint32_t b = blockIdx.x / P.tiles, p = blockIdx.x % P.tiles;
     const uint32_t lane = lane_id(), wave = threadIdx.x / kWave;
     const uint32_t col = p * kScanTile + threadIdx.x * 4u;
-    // the parse kernel's matrix is chunk-major: bucket b of chunk c at c nb + b
-    const size_t cb = (size_t)col * P.nb + b;
-    uint4 v;
-    v.x = col + 0u < P.nchunk ? P.cnt[cb] : 0u;
-    v.y = col + 1u < P.nchunk ? P.cnt[cb + P.nb] : 0u;
-    v.z = col + 2u < P.nchunk ? P.cnt[cb + 2u * P.nb] : 0u;
-    v.w = col + 3u < P.nchunk ? P.cnt[cb + 3u * P.nb] : 0u;
+    const uint4 *row = reinterpret_cast<const uint4 *>(P.cnt + (size_t)b * P.ncol);
+    uint4 v = row[col / 4u];
     // columns past the last chunk were never written this launch
     if (col + 0u >= P.nchunk) v.x = 0;
     if (col + 1u >= P.nchunk) v.y = 0;
@@ -1221,7 +1149,6 @@ __global__ __launch_bounds__(kScatterBlock, 4) void yrss_scatter(ScatterParams P
 // _LIST_RANGE / _COUNT_MISMATCH).
 // ---------------------------------------------------------------------------
 constexpr int kLineBlock = 512;
-constexpr uint32_t kMaxLineGrid = 1024;   // line scatter workgroups (look-back granules)
 // s_waitcnt vmcnt(0), expcnt and lgkmcnt left alone (gfx9 encoding)
 constexpr int kWaitVm0 = 0x0F70;
 // prefix words a thread holds: the table is nb x span chunks <= 512 x regs
@@ -1239,10 +1166,8 @@ constexpr uint32_t line_span_max(uint32_t g) { return kLineBlock * 8u * g; }
 struct LineParams {
     const int16_t *q;          // !kPacked: the bucket of each packet
     const uint16_t *rank;      // rank in chunk (kPacked: bucket << cshift | rank)
-    const uint32_t *cnt;       // [ncol][nb] per-chunk counts, chunk-major (the parse kernel's)
-    const uint32_t *tot8;      // [8][nb] the batch's per-bucket counts of each region
-    unsigned long long *agg1;  // [grid][nb] range aggregates: epoch << 32 | count
-    unsigned long long *agg2;  // [grid][nb] group aggregates, at the group's first range
+    const uint32_t *seg_off;   // [nb][ncol] exclusive per-bucket prefix per chunk
+    const uint32_t *totals;    // [nb]
     uint32_t *qidx;
     uint32_t *qstart;          // [nb + 1]
     uint32_t *fault;
@@ -1251,16 +1176,12 @@ struct LineParams {
     uint32_t gshift, cshift;   // span = 2^gshift chunks, chunk = 2^cshift packets
     uint32_t lmax;             // stage lines: seg / 16 + 2 nb + 1
     uint32_t xcd;              // workgroups of one XCD take consecutive ranges
-    uint32_t epoch;            // the batch's tag in agg1 / agg2 (31 bits, never 0)
-    uint32_t reg_lo[9];        // region x = logical ranges [reg_lo[x], reg_lo[x + 1])
-    uint32_t wait_ticks;       // look-back patience (s_memrealtime) before computing a
-                               // missing aggregate from the counts itself
 };
 
 // LDS of a workgroup, in words: per-bucket arrays, the prefix table, the
 // carried lines, the stage's line tags, the stage (+ a spare word).
 struct LineLds {
-    uint32_t start, cs, ve, ce, so, rb, lsl, st, misc, tab, cb, ltag, lgl, stg, words;
+    uint32_t start, cs, ve, ce, so, rb, lsl, misc, tab, cb, ltag, lgl, stg, words;
 };
 __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32_t lmax)
 {
@@ -1279,7 +1200,6 @@ __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32
     L.so = take(2u * nb);    // stage index = so[b] + adjusted position
     L.rb = take(2u * nb);    // prefix table row bias (to stage slots)
     L.lsl = take(2u * (nb + 1u));   // first stage line of each bucket
-    L.st = take(2u * nb);    // the span's packets per bucket (row totals of its counts)
     L.misc = take(8);
     L.tab = take(nb * ((1u << gshift) + 1u));   // rows of 2^gshift + 1 words (odd: banks)
     L.cb = take(16u * nb);
@@ -1336,12 +1256,6 @@ __device__ uint64_t g_line_prof[2048 * 8 * 8];
     } while (0)
 #endif
 
-#ifdef YRSS_LB_STATS
-// measurement builds only: [0] workgroups started, [1] finished, [2] the most
-// finished seen by a starting one, [3] look-back fallbacks taken
-__device__ uint32_t g_lb_stats[8];
-#endif
-
 template <bool kPacked, uint32_t kG>
 __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lines(LineParams P)
 {
@@ -1364,19 +1278,24 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // list position x is "adjusted" a = x + ph: 64-byte lines are a >> 4
     const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 15u);
 
-    // The batch's per-bucket totals: the parse kernel's workgroups added
-    // theirs into 8 shards.  List starts (exclusive scan of the totals);
-    // workgroup 0 also writes qstart.
+    // list starts (exclusive scan of totals); workgroup 0 also writes qstart.
+    // Every bucket block's total is loaded before the first is scanned: one
+    // round trip, not one per 64 buckets.
     if (wave == 0) {
-        uint32_t carry = 0, nzb = 0;
-        for (uint32_t b0 = 0; b0 < nb; b0 += kWave) {
-            const uint32_t b = b0 + lane;
-            uint32_t x0 = 0;
-            if (b < nb)
+        constexpr uint32_t kTB = kG == 2u ? 2u : 8u;   // nb <= 64 kTB
+        uint32_t tv[kTB];
 #pragma unroll
-                for (uint32_t k = 0; k < 8u; ++k)
-                    x0 += __hip_atomic_load(P.tot8 + k * nb + b, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t i = 0; i < kTB; ++i) {
+            const uint32_t b = i * kWave + lane;
+            tv[i] = i * kWave < nb && b < nb ? P.totals[b] : 0u;
+        }
+        uint32_t carry = 0, nzb = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kTB; ++i) {
+            if (i * kWave >= nb)   // (uniform)
+                break;
+            const uint32_t b = i * kWave + lane;
+            const uint32_t x0 = tv[i];
             nzb += (uint32_t)__popcll(__ballot(x0 != 0u));
             const uint32_t x = wave_incl_scan(x0, lane);
             if (b < nb) {
@@ -1392,8 +1311,6 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             misc[0] = nzb;
             misc[1] = 0u;
             misc[3] = 0u;
-            if (carry != P.n)   // every packet is in exactly one bucket
-                report_fault(P.fault, YRSS_FAULT_COUNT_MISMATCH, YRSS_K_SCATTER, 0xffffffffu, carry);
         }
     }
     __syncthreads();
@@ -1422,206 +1339,25 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // this workgroup's range of spans
     const uint32_t nsp = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
     const uint32_t r = xcd_block(P.xcd), G = gridDim.x;
-    auto range_of = [&](uint32_t m, uint32_t &a, uint32_t &e) {
-        a = (uint32_t)((uint64_t)m * nsp / G);
-        e = (uint32_t)((uint64_t)(m + 1u) * nsp / G);
-    };
-    uint32_t g0, g1;
-    range_of(r, g0, g1);
+    const uint32_t g0 = (uint32_t)((uint64_t)r * nsp / G);
+    const uint32_t g1 = (uint32_t)((uint64_t)(r + 1u) * nsp / G);
+    if (g0 >= g1)
+        return;
     // prefix table rows are ncs + 1 words apart: with a power-of-two row the
     // lanes of one chunk column hit one or two LDS banks whatever their bucket
     // (a 0.78 conflict share of the LDS cycles at 64 buckets)
     const uint32_t ncs = 1u << P.gshift, ntab = nb << P.gshift, rs = ncs + 1u;
+    auto prefix = [&](uint32_t b, uint32_t c) {
+        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : P.totals[b];
+    };
     auto span_end = [&](uint32_t g) {
         const uint64_t e = (uint64_t)g * P.seg + P.seg;
         return e < P.n ? (uint32_t)e : P.n;
     };
-    const __amdgpu_buffer_rsrc_t rcnt = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t *>(P.cnt), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
-    // sum of counts of bucket b over the chunk columns of spans [a, e)
-    // (one thread: the look-back's fallback)
-    auto count_cols = [&](uint32_t b, uint32_t a, uint32_t e) {
-        const uint32_t c1 = min(e << P.gshift, P.nchunk);
-        uint32_t sum = 0;
-        for (uint32_t c = a << P.gshift; c < c1; ++c)
-            sum += __builtin_amdgcn_raw_buffer_load_b32(rcnt, (int)(b * 4u), (int)(c * nb * 4u), 0);
-        return sum;
-    };
-
-    // ---- the range's prefix per bucket, without a scan kernel ------------
-    // (1) the range's own counts, summed per bucket (lagg), published as
-    //     agg1[r][b] = epoch << 32 | sum (one 8-byte granule: tag and value
-    //     can not tear);
-    // (2) each group of 16 consecutive ranges: its last range also sums the
-    //     group (agg2[r / 16][b]) once it has its members' agg1;
-    // (3) prefix (lpre) = agg2 of every earlier group + agg1 of every earlier
-    //     range of this group: at most 15 + G / 16 values a bucket, read at
-    //     once, so no range waits on a chain of inclusive prefixes (the
-    //     chained look-back, every range resident at once, resolved one range
-    //     per round trip: 43 us).
-    // Every workgroup is normally resident (the grid is the resident count),
-    // so every value it waits for is published a round trip or two after
-    // the launch.  A value still missing after wait_ticks (another kernel
-    // holding CUs, so a range has not started) is summed from the count
-    // matrix by the waiting thread itself: the wait is bounded and the
-    // answer does not depend on which happened.
-    uint32_t *lagg = stg, *lpre = stg + nb, *rbase = stg + 2u * nb;
-    // the region (the ranges of one XCD) holding this range; every earlier
-    // region's counts come whole from the parse kernel's region totals
-    uint32_t xr = 0;
-#pragma unroll
-    for (uint32_t i = 1; i < 8u; ++i)
-        xr += r >= P.reg_lo[i] ? 1u : 0u;
-    const uint32_t rlo = P.reg_lo[xr], rhi = P.reg_lo[xr + 1u];
-#ifdef YRSS_LB_STATS
-    if (t == 0) {
-        atomicAdd(&g_lb_stats[0], 1u);
-        atomicMax(&g_lb_stats[2], __hip_atomic_load(&g_lb_stats[1], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT));
-    }
-#endif
-    for (uint32_t b = t; b < nb; b += kLineBlock) {
-        uint32_t base = 0;
-        for (uint32_t x = 0; x < xr; ++x)
-            base += __hip_atomic_load(P.tot8 + x * nb + b, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-        lagg[b] = 0u;
-        lpre[b] = 0u;
-        rbase[b] = base;
-    }
-    __syncthreads();
-    {
-        // the range's chunks are one contiguous stretch of the chunk-major
-        // matrix: element e is bucket e mod nb
-        const uint32_t c_lo = g0 << P.gshift, c_hi = min(g1 << P.gshift, P.nchunk);
-        const uint32_t total = c_hi > c_lo ? (c_hi - c_lo) * nb : 0u;
-        if (total) {
-            constexpr uint32_t kAR = 16;   // loads in flight a thread
-            const uint32_t r512 = kLineBlock % nb;
-            const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint32_t *>(P.cnt + (size_t)c_lo * nb), 0, (int)(total * 4u), kRsrcWord3);
-            uint32_t b = t % nb;
-            for (uint32_t e0 = 0; e0 < total; e0 += kLineBlock * kAR) {
-                uint32_t v[kAR], bk[kAR];
-#pragma unroll
-                for (uint32_t i = 0; i < kAR; ++i) {
-                    v[i] = __builtin_amdgcn_raw_buffer_load_b32(
-                        rr, (int)((e0 + i * kLineBlock + t) * 4u), 0, 0);   // past total: 0
-                    bk[i] = b;
-                    b += r512;
-                    if (b >= nb)
-                        b -= nb;
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < kAR; ++i)
-                    if (v[i])
-                        atomicAdd(&lagg[bk[i]], v[i]);
-            }
-        }
-    }
-    __syncthreads();
-    const unsigned long long tag = (unsigned long long)(P.epoch & 0x7fffffffu) << 32;
-    for (uint32_t b = t; b < nb; b += kLineBlock)
-        __hip_atomic_store(P.agg1 + (size_t)r * nb + b, tag | lagg[b], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    // groups of 16 consecutive ranges from the region's first: every value a
-    // range waits for comes from a range of its own region with a lower index,
-    // i.e. (XCD-contiguous mapping, xcd_block) a workgroup with a lower
-    // blockIdx, dispatched before it
-    const uint32_t grp = (r - rlo) >> 4, first = rlo + (grp << 4);
-    const uint32_t lastm = min(first + 15u, rhi - 1u);
-    const uint64_t deadline = wall_clock64() + P.wait_ticks;
-    // waits for granule w of this batch; past the deadline, computes it
-    auto take = [&](unsigned long long *w, uint32_t b, uint32_t a, uint32_t e) -> uint32_t {
-        for (;;) {
-#ifdef YRSS_LB_RMW
-            const unsigned long long x = __hip_atomic_fetch_or(w, 0ull, __ATOMIC_RELAXED,
-                                                               __HIP_MEMORY_SCOPE_AGENT);
-#else
-            const unsigned long long x = __hip_atomic_load(w, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-#endif
-            if ((x & ~0xffffffffull) == tag)
-                return (uint32_t)x;
-            if (wall_clock64() > deadline) {
-#ifdef YRSS_LB_STATS
-                atomicAdd(&g_lb_stats[3], 1u);
-#endif
-                return count_cols(b, a, e);
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    };
-    // entries e < cnt_e (granule, bucket, spans it sums): every granule of a
-    // pass is loaded before any is waited for, so a pass costs one round trip
-    auto gather = [&](uint32_t cnt_e, bool grp_src) {
-        constexpr uint32_t kLB = 16;
-        for (uint32_t e0 = 0; e0 < cnt_e; e0 += kLineBlock * kLB) {
-            unsigned long long x[kLB];
-#pragma unroll
-            for (uint32_t i = 0; i < kLB; ++i) {
-                const uint32_t e = e0 + i * kLineBlock + t;
-                x[i] = 0ull;
-                if (e < cnt_e) {
-                    const uint32_t m = e / nb, b = e - m * nb;
-                    unsigned long long *w = grp_src ? P.agg2 + (size_t)(rlo + 16u * m) * nb + b
-                                                    : P.agg1 + (size_t)(first + m) * nb + b;
-#ifdef YRSS_LB_RMW
-                    x[i] = __hip_atomic_fetch_or(w, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-                    x[i] = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-                }
-            }
-#pragma unroll
-            for (uint32_t i = 0; i < kLB; ++i) {
-                const uint32_t e = e0 + i * kLineBlock + t;
-                if (e >= cnt_e)
-                    continue;
-                const uint32_t m = e / nb, b = e - m * nb;
-                uint32_t v;
-                if ((x[i] & ~0xffffffffull) == tag) {
-                    v = (uint32_t)x[i];
-                } else {
-                    uint32_t sa, se, za, ze;
-                    if (grp_src) {
-                        range_of(rlo + 16u * m, sa, se);
-                        range_of(min(rlo + 16u * m + 15u, rhi - 1u), za, ze);
-                    } else {
-                        range_of(first + m, sa, ze);
-                    }
-                    v = take(grp_src ? P.agg2 + (size_t)(rlo + 16u * m) * nb + b
-                                     : P.agg1 + (size_t)(first + m) * nb + b,
-                             b, sa, ze);
-                }
-                if (v)
-                    atomicAdd(&lpre[b], v);
-            }
-        }
-    };
-    gather((r - first) * nb, false);   // agg1 of this group's earlier ranges
-    if (r == lastm) {
-        __syncthreads();
-        for (uint32_t b = t; b < nb; b += kLineBlock)
-            __hip_atomic_store(P.agg2 + (size_t)first * nb + b,
-                               tag | (lpre[b] + lagg[b]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();   // lpre read above before the groups' values go in
-    }
-    gather(grp * nb, true);            // agg2 of every earlier group
-    if (g0 >= g1)
-        return;   // (a range always holds a span: the grid is at most the spans)
-#ifdef YRSS_PROF_LINES
-    if (t == 0 && blockIdx.x < 2048u)   // look-back done, slot 6 of span 0
-        g_line_prof[(blockIdx.x * 8u) * 8u + 6u] = __builtin_amdgcn_s_memrealtime();
-#endif
-    __syncthreads();
-    // set 1 holds the state before the range's first span (set 0)
-    for (uint32_t b = t; b < nb; b += kLineBlock) {
-        const uint32_t a = start[b] + rbase[b] + lpre[b] + ph;
-        cs[nb + b] = a;
-        ve[nb + b] = a;
-    }
+    // set 1 holds the state before the range's first span (set 0): its
+    // prefixes are loaded beside the first span's streams (one round trip for
+    // both) and written once they have arrived
+    const uint32_t pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
     const ListOut lout = list_out(P.qidx, P.n);
     // The span's streams alternate between two register sets: span g+1's
     // loads issue at the start of span g's phase (b), once its table is in
@@ -1631,48 +1367,56 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // too (their write-through acks), and a load issued after the place phase
     // had only the copy-out to hide its latency.
     u32x4 pkA[kG], qkA[kG], pkB[kG], qkB[kG];
+    // wave 0 also holds, a bucket to a lane, each bucket's prefix at the
+    // span's first chunk and at its end, so it lays the span out from
+    // registers while the other waves write the prefix table
     constexpr uint32_t kBI = kG == 2u ? 2u : 8u;   // nb <= 64 kBI
     constexpr uint32_t kLineTabRegs = line_tab_regs(kG);
-    // the span's chunk counts, element k * 512 + t = row (t >> gshift) + k *
-    // (512 >> gshift), column t & (ncs - 1): after scan_span, each one's
-    // exclusive prefix inside the span
-    uint32_t pt[kLineTabRegs];
+    uint32_t pt[kLineTabRegs], w0s[kBI], w0e[kBI];
     auto load_span = [&](uint32_t g, u32x4 (&pk)[kG], u32x4 (&qk)[kG]) {
         const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
         load_groups(P.rank, p0, pe, tt, pk);
         if (!kPacked)
             load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, qk);
         const uint32_t c0 = g << P.gshift;
-        // (bucket, chunk) at (c0 + chunk) nb + bucket of the chunk-major
-        // matrix; rows past nb and columns past the last chunk are masked in
-        // scan_span.  One load form on every path: a plain load on a rare path
-        // left a pending destination register that the compiler later waited
-        // for with vmcnt(0), i.e. for every list store in flight.
-        const uint32_t vo = ((tt & (ncs - 1u)) * nb + (tt >> P.gshift)) * 4u;
-        const uint32_t step = (kLineBlock >> P.gshift) * 4u;
+        if (wave == 0) {
+            // rows past nb read 0 (range check); a span's end past the last
+            // chunk is the bucket's total
+            const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
+            const __amdgpu_buffer_rsrc_t rtot = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint32_t *>(P.totals), 0, (int)(nb * 4u), kRsrcWord3);
+            const bool inner = c0 + ncs < P.nchunk;
+            const uint32_t ll = opaque(lane);
+#pragma unroll
+            for (uint32_t i = 0; i < kBI; ++i) {
+                if (i * kWave < nb) {   // (uniform)
+                    const uint32_t b = i * kWave + ll;
+                    w0s[i] = __builtin_amdgcn_raw_buffer_load_b32(rs0, (int)(b * P.ncol * 4u),
+                                                                  (int)(c0 * 4u), 0);
+                    w0e[i] = inner ? __builtin_amdgcn_raw_buffer_load_b32(
+                                         rs0, (int)(b * P.ncol * 4u), (int)((c0 + ncs) * 4u), 0)
+                                   : __builtin_amdgcn_raw_buffer_load_b32(rtot, (int)(b * 4u), 0, 0);
+                }
+            }
+        }
+        // element k * 512 + t is row (t >> gshift) + k * (512 >> gshift),
+        // column t & (ncs - 1), so one per-lane offset and a scalar step per
+        // k; rows past nb read 0 (range check).  Columns past the last chunk
+        // (a batch's last span) read whatever the matrix holds there: no
+        // packet's slot uses them.  One load form on every path: a plain
+        // load on a rare path left a pending destination register that the
+        // compiler later waited for with vmcnt(0), i.e. for every list store
+        // in flight.
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
+        const uint32_t vo = ((tt >> P.gshift) * P.ncol + (tt & (ncs - 1u))) * 4u;
+        const uint32_t step = (kLineBlock >> P.gshift) * P.ncol * 4u;
 #pragma unroll
         for (uint32_t k = 0; k < kLineTabRegs; ++k)
             if (k * kLineBlock < ntab)   // (uniform)
-                pt[k] = __builtin_amdgcn_raw_buffer_load_b32(rcnt, (int)vo,
-                                                             (int)(c0 * nb * 4u + k * step), 0);
-    };
-    // After span g's loads arrived: each count becomes its exclusive prefix
-    // inside the span (a segmented scan over the row's ncs lanes), and each
-    // row's total (the span's packets of that bucket) goes to st[s][b].
-    auto scan_span = [&](uint32_t g, uint32_t s) {
-        const uint32_t tt = opaque(t), col = tt & (ncs - 1u);
-        const bool live = (g << P.gshift) + col < P.nchunk;
-#pragma unroll
-        for (uint32_t k = 0; k < kLineTabRegs; ++k) {
-            if (k * kLineBlock < ntab) {   // (uniform)
-                const uint32_t row = (tt >> P.gshift) + k * (kLineBlock >> P.gshift);
-                const uint32_t x = live && row < nb ? pt[k] : 0u;
-                const uint32_t inc = seg_incl_scan(x, lane, ncs);
-                pt[k] = inc - x;
-                if (col == ncs - 1u && row < nb)
-                    lsm[o.st + s * nb + row] = inc;
-            }
-        }
+                pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo,
+                                                             (int)(c0 * 4u + k * step), 0);
     };
     load_span(g0, pkA, qkA);
     // the first span's loads waited for here, so that at the loop head no
@@ -1680,16 +1424,19 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // vmcnt(0) at the prefix table's first use in every span, i.e. for the
     // previous span's list stores as well
     __builtin_amdgcn_s_waitcnt(kWaitVm0);
-    scan_span(g0, 0u);
+    if (t < nb) {
+        const uint32_t a = start[t] + pre0 + ph;
+        cs[nb + t] = a;
+        ve[nb + t] = a;
+    }
     // Wave 0, a bucket to a lane, lays span g out into set s from set s ^ 1
-    // and the span's packets per bucket (st): the valid positions [cs, ve) =
+    // and the prefixes it holds (w0s, w0e): the valid positions [cs, ve) =
     // the carried words and the span's packets, the bucket's stage lines
-    // (exclusive scan), its stage offset so and the bias rb from a prefix
-    // inside the span to a stage slot.  Span g + 1's layout is made during
-    // span g's copy-out, so a span starts with its layout in place.
+    // (exclusive scan), its stage offset so and the bias rb from a prefix to
+    // a stage slot.  Span g + 1's layout is made during span g's copy-out,
+    // so a span starts with its layout in place.
     auto layout = [&](uint32_t g, uint32_t s) {
         const uint32_t *pcs = cs + (s ^ 1u) * nb, *pve = ve + (s ^ 1u) * nb;
-        const uint32_t *pst = lsm + o.st + s * nb;
         uint32_t *wcs = cs + s * nb, *wve = ve + s * nb, *wce = ce + s * nb, *wso = so + s * nb;
         uint32_t *wrb = rb + s * nb, *wlsl = lsl + s * (nb + 1u);
         uint32_t lines = 0;
@@ -1705,7 +1452,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             if (b < nb) {
                 e0 = pve[b];
                 v0 = max(pcs[b], e0 & ~15u);
-                const uint32_t e1 = e0 + pst[b];
+                const uint32_t e1 = e0 + (w0e[i] - w0s[i]);
                 wcs[b] = v0;
                 wce[b] = e0;
                 wve[b] = e1;
@@ -1716,7 +1463,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 const uint32_t l0 = lines + x - nl;
                 wlsl[b] = l0;
                 wso[b] = 16u * (l0 - (v0 >> 4));
-                wrb[b] = 16u * (l0 - (v0 >> 4)) + e0;
+                wrb[b] = 16u * (l0 - (v0 >> 4)) + e0 - w0s[i];
             }
             lines += __shfl(x, kWave - 1, kWave);
         }
@@ -1729,7 +1476,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             misc[4u + s] = lines;
         }
     };
-    __syncthreads();   // set 1 and the first span's row totals written
+    __syncthreads();   // set 1 written
     if (wave == 0)
         layout(g0, 0u);
     __syncthreads();
@@ -1833,12 +1580,10 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         else
             place(std::true_type{});
         LPROF(2);
-        // the next span's streams and counts (issued in (b)) have arrived;
+        // the next span's streams and prefixes (issued in (b)) have arrived;
         // waiting here, before this span's list stores, keeps those stores
         // out of the next wait (vmcnt counts loads and stores in one queue)
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        if (!last)
-            scan_span(g + 1u, s ^ 1u);   // its prefixes, and the row totals wave 0 lays it out by
         __syncthreads();
         LPROF(3);
         // (c) copy-out, a quad per thread: whole lines as 16-byte non-temporal
@@ -1921,10 +1666,6 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         if (g + 1u < g1)
             span(g + 1u, 1u, pkB, qkB, pkA, qkA);
     }
-#ifdef YRSS_LB_STATS
-    if (t == 0)
-        atomicAdd(&g_lb_stats[1], 1u);
-#endif
     // every packet of the range left exactly once
     wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
     wsum = __shfl(wave_incl_scan(wsum, lane), kWave - 1, kWave);
@@ -2791,13 +2532,6 @@ struct yrss_ctx {
         uint32_t *totals = nullptr;
         unsigned long long *scan_status = nullptr;   // [nb][kMaxChunks / kScanTile]
         uint32_t scan_epoch = 0;
-        // the line scatter's inputs besides the counts: the batch's totals
-        // (two parities of 8 shards x nb, tot_words apart) and its look-back
-        // granules (agg1 [kMaxLineGrid][nb], then agg2 [kMaxLineGrid][nb])
-        uint32_t *tot8 = nullptr;
-        uint32_t tot_words = 0, tpar = 0;
-        unsigned long long *agg = nullptr;
-        uint32_t line_epoch = 0;
         uint16_t *rank = nullptr;    // n x u16, grown on demand
         size_t rank_cap = 0;
     };
@@ -3311,14 +3045,6 @@ hipError_t list_ws_alloc(yrss_ctx *c, yrss_ctx::ListWs &w)
         (e = hipMemset(w.scan_status, 0, st)) != hipSuccess ||
         (e = hipMemset(w.seg_cnt, 0, cnt)) != hipSuccess)
         return e;
-    w.tot_words = (8u * c->nb + 63u) & ~63u;   // each parity on lines of its own
-    // agg1 rows, then agg2 rows (indexed by a group's first range: up to kMaxLineGrid)
-    const size_t ag = (size_t)(2u * kMaxLineGrid) * c->nb * sizeof(unsigned long long);
-    if ((e = hipMalloc((void **)&w.tot8, 2u * w.tot_words * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMemset(w.tot8, 0, 2u * w.tot_words * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMalloc((void **)&w.agg, ag)) != hipSuccess ||
-        (e = hipMemset(w.agg, 0, ag)) != hipSuccess)
-        return e;
     return hipSuccess;
 }
 
@@ -3328,8 +3054,6 @@ void list_ws_free(yrss_ctx::ListWs &w)
     (void)hipFree(w.seg_off);
     (void)hipFree(w.totals);
     (void)hipFree(w.scan_status);
-    (void)hipFree(w.tot8);
-    (void)hipFree(w.agg);
     (void)hipFree(w.rank);
     w = yrss_ctx::ListWs{};
 }
@@ -3815,31 +3539,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     // the line scatter reads q (when the bucket is not packed with the rank)
     // as 16-byte vectors
     const bool ranked = compact && lp.ok && (lp.packed || ((uintptr_t)b->q & 15u) == 0);
-    // The line scatter: persistent, the resident workgroups, each one
-    // contiguous range of spans, never more workgroups than spans.  Its
-    // ranges fall into 8 regions, one per XCD (xcd_block), and the parse
-    // kernel totals each region's counts per bucket, so a range's prefix is
-    // the earlier regions' totals plus a look-back inside its own region.
-    void (*line_fn)(LineParams) =
-        lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
-                        : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
-    uint32_t sgrid = 1, reg_lo[9] = {0}, reg_col[8] = {0};
-    for (uint32_t x = 1; x < 8u; ++x)
-        reg_col[x] = 0xffffffffu;   // one region (no line scatter: unused)
-    if (ranked) {
-        const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
-        sgrid = std::max(1u, std::min({spans, resident_blocks(c, (const void *)line_fn, kLineBlock,
-                                                              lp.lds),
-                                       kMaxLineGrid}));
-        const bool xon = c->tune.scatter_xcd != 0 && sgrid >= 16u;   // as xcd_block
-        const uint32_t per = sgrid >> 3, rem = sgrid & 7u;
-        for (uint32_t x = 0; x <= 8u; ++x)
-            reg_lo[x] = xon ? std::min(sgrid, x * per + std::min(x, rem)) : (x ? sgrid : 0u);
-        for (uint32_t x = 1; x < 8u; ++x) {
-            const uint64_t sp = (uint64_t)reg_lo[x] * spans / sgrid;   // as range_of
-            reg_col[x] = (uint32_t)std::min<uint64_t>(sp << lp.gshift, 0xffffffffu);
-        }
-    }
     if (ranked && W.rank_cap < n) {
         // the ranks' workspace grows to the largest batch seen; the old one
         // may still be read by a scatter queued on this stream
@@ -3870,15 +3569,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
     P.rank_pack = ranked && lp.packed ? 1u : 0u;
-    // the batch's totals go to parity tpar; the parse kernel zeroes the
-    // other parity for the next batch (the previous batch, which read it, is
-    // done: same stream, or ordered by switch_ev above)
-    const uint32_t tpar = W.tpar;
-    if (compact) {
-        P.tot_add = W.tot8 + (size_t)tpar * W.tot_words;
-        P.tot_zero = W.tot8 + (size_t)(tpar ^ 1u) * W.tot_words;
-        memcpy(P.reg_col, reg_col, sizeof(reg_col));
-    }
     {
         Timed t(c, YRSS_K_PARSE_HASH);
         hipExtLaunchKernelGGL(pick_parse(ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
@@ -3888,14 +3578,10 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     YRSS_HIP(hipGetLastError());
     if (!compact)
         return 0;
-    W.tpar ^= 1u;   // launched: the next batch adds into the parity zeroed here
-    // the line scatter resolves its own prefixes (no scan kernel); the
-    // large-batch fallback scatter still reads the scan's per-chunk prefixes
-    if (!ranked) {
+    {
         Timed t(c, YRSS_K_SCAN);
         ScanParams SP;
         SP.cnt = W.seg_cnt;
-        SP.nb = c->nb;
         SP.off = W.seg_off;
         SP.totals = W.totals;
         SP.status = W.scan_status;
@@ -3914,18 +3600,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         LineParams S;
         S.q = b->q;
         S.rank = W.rank;
-        S.cnt = W.seg_cnt;
-        S.tot8 = W.tot8 + (size_t)tpar * W.tot_words;
-        S.agg1 = W.agg;
-        S.agg2 = W.agg + (size_t)kMaxLineGrid * c->nb;
-        if ((++W.line_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
-            ++W.line_epoch;
-        S.epoch = W.line_epoch;
-#ifdef YRSS_LB_WAIT
-        S.wait_ticks = YRSS_LB_WAIT;
-#else
-        S.wait_ticks = 100u * 100u;   // 100 us at the 100 MHz s_memrealtime clock
-#endif
+        S.seg_off = W.seg_off;
+        S.totals = W.totals;
         S.qidx = b->qidx;
         S.qstart = b->qstart;
         S.fault = c->d_fault_rec;
@@ -3939,9 +3615,17 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         S.cshift = lay.ct_shift + 6u;
         S.lmax = lp.lmax;
         S.xcd = c->tune.scatter_xcd != 0 ? 1u : 0u;
-        memcpy(S.reg_lo, reg_lo, sizeof(reg_lo));
+        // persistent: the resident workgroups, each one contiguous range of
+        // spans, never more workgroups than spans
+        const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
+        void (*fn)(LineParams) =
+            lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
+                            : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
+        const uint32_t sgrid =
+            std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
         Timed t(c, YRSS_K_SCATTER);
-        hipExtLaunchKernelGGL(line_fn, dim3(sgrid), dim3(kLineBlock), lp.lds, s, t.a, t.b, 0, S);
+        hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(kLineBlock), lp.lds, s, t.a,
+                              t.b, 0, S);
         YRSS_HIP(hipGetLastError());
         return 0;
     }
@@ -3982,22 +3666,6 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
 }  // namespace
 
 extern "C" {
-
-#ifdef YRSS_LB_STATS
-// measurement builds only: the line scatter's residency / look-back counters
-// (read, then cleared)
-int yrss_debug_lb_stats(uint32_t *out)
-{
-    uint32_t z[8] = {0};
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lb_stats), sizeof(z), 0, hipMemcpyDeviceToHost) !=
-            hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(g_lb_stats), z, sizeof(z), 0, hipMemcpyHostToDevice) !=
-            hipSuccess)
-        return -EIO;
-    return 0;
-}
-#endif
 
 #ifdef YRSS_PROF_LINES
 // measurement builds only: the line scatter's phase clock (tools/line_prof.py)
