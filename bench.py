@@ -502,6 +502,7 @@ def pcie_inclusive(profile: str, place=None):
     # burst and the thread's and pool's NUMA placement beside the GPU's.
     for frames, burst, blocks in (("0", 32, 128), ("0", 1024, 32), ("1", 32, 128),
                                   ("1", 1024, 32), ("2", 32, 128), ("2", 1024, 32)):
+        print(f"pcie_inclusive: worker form {frames}, burst {burst}", file=sys.stderr, flush=True)
         try:
             r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
@@ -548,6 +549,7 @@ def pcie_fanout(profile: str, world: int, place=None):
     one = bool(os.environ.get("YRSS_BENCH_ONE_DEVICE"))   # rehearsal: N contexts, device 0
     devs = ",".join("0" if one else str(d) for d in range(world))
     for frames, burst, blocks in (("1", 32, 128), ("1", 1024, 32), ("0", 32, 128)):
+        print(f"pcie_fanout: form {frames}, burst {burst}", file=sys.stderr, flush=True)
         try:
             r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
