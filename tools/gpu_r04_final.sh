@@ -40,6 +40,10 @@ if [ "${PART:-all}" = c ]; then
     step rehearse_n8_vlan6 620 bash tools/gpu_rehearse.sh 8 vlan6_tcp || exit 1
     step rehearse_n8_jumbo 620 bash tools/gpu_rehearse.sh 8 jumbo_tcp4 || exit 1
     step configs 900 python tools/configs_table.py || exit 1
+    # last (a host SIGSEGV ends the call): can the host write device memory?
+    for m in 0 1 2; do
+        step bar_probe_$m 60 tools/bar_probe $m || exit 1
+    done
     echo "== done (part c)"
     exit 0
 fi
