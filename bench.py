@@ -425,9 +425,12 @@ def _cpulist(text: str):
 
 def gpu_placement(device: str):
     """NUMA node of the GPU (PCI address from device_identity) and the CPU the
-    host-resident dispatcher thread is pinned to: the first CPU of that node
-    this process may run on (the reference's dispatching lcore sits beside its
-    NIC and GPU).  None where sysfs does not say."""
+    host-resident dispatcher thread is pinned to: a CPU of that node this
+    process may run on, from the middle of the node's list rather than its
+    first (CPU 0 takes the box's housekeeping: the windows form's copy ran at
+    1256-1440 cycles a burst there, profiles/r04_final_bench.log); the
+    reference's dispatching lcore sits beside its NIC and GPU.  None where
+    sysfs does not say."""
     node, cpu = None, None
     try:
         node = int(Path(f"/sys/bus/pci/devices/{device}.0/numa_node").read_text())
@@ -438,7 +441,7 @@ def gpu_placement(device: str):
         try:
             local = _cpulist(Path(f"/sys/devices/system/node/node{node}/cpulist").read_text())
             mine = [c for c in local if c in set(allowed)]
-            cpu = mine[0] if mine else None
+            cpu = mine[len(mine) // 2] if mine else None
         except (OSError, ValueError):
             cpu = None
     return {"gpu_node": node, "dispatch_cpu": cpu}

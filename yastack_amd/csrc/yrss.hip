@@ -666,8 +666,10 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
             const uint32_t j = e / per_round, r = e - j * per_round;
             const uint32_t b = r / kWaves, w = r - b * kWaves;
             const uint32_t col = g0 + w + j * W;
+#ifndef YRSS_NO_CNT_FLUSH   // measurement builds only: the flush's cost (lists then wrong)
             if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords)
                 P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
+#endif
         }
     }
 }
