@@ -134,6 +134,15 @@ def test_many_buckets_large_chunks(dev, oracle_mod, cfg):
         check(eng, oracle_mod, cfg, abi.SYN_TCP4, 1 << 25, first=17)
 
 
+@pytest.mark.parametrize("cfg", [(255, 255, 1, 0), (200, 200, 1, 1)])
+def test_many_buckets_two_chunks_a_wave(dev, oracle_mod, cfg):
+    """Past 128 buckets chunks grow with the batch up to 64 tiles, two a parse
+    wave at 2^24 (layout_for): a ragged batch just past 2^24, fuzz traffic,
+    compared in full."""
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        check(eng, oracle_mod, cfg, abi.SYN_FUZZ, (1 << 24) + 12345, first=23)
+
+
 @pytest.mark.parametrize("profile", [abi.SYN_UDP4, abi.SYN_TCP4, abi.SYN_IMIX])
 @pytest.mark.parametrize("shift", [1, 2, 3])
 def test_unaligned_list_outputs(oracle_mod, profile, shift):

@@ -661,15 +661,29 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         __syncthreads();
         const uint32_t g0 = blockIdx.x * kWaves;
         const uint32_t kmax = P.nchunk > g0 ? (P.nchunk - g0 + W - 1) / W : 0u;
-        const uint32_t per_round = kWaves * P.nb;
-        for (uint32_t e = threadIdx.x; e < kmax * per_round; e += kBlock) {
-            const uint32_t j = e / per_round, r = e - j * per_round;
-            const uint32_t b = r / kWaves, w = r - b * kWaves;
+        // element e = (j * nb + b) * kWaves + w; the block size is a multiple
+        // of kWaves, so a thread keeps its wave w and steps m = j * nb + b by
+        // kBlock / kWaves, carried into (j, b) without a division.  The flush
+        // costs ~5 us at 65 and 256 buckets, ~0 at 4 (a build without it,
+        // profiles/r04_cntflush_ab.log).
+        static_assert(kBlock % kWaves == 0, "a thread keeps its wave");
+        const uint32_t w = threadIdx.x % kWaves;
+        uint32_t j = 0, b = threadIdx.x / kWaves;
+        while (b >= P.nb) {
+            b -= P.nb;
+            ++j;
+        }
+        while (j < kmax) {
             const uint32_t col = g0 + w + j * W;
 #ifndef YRSS_NO_CNT_FLUSH   // measurement builds only: the flush's cost (lists then wrong)
             if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords)
                 P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
 #endif
+            b += kBlock / kWaves;
+            while (b >= P.nb) {
+                b -= P.nb;
+                ++j;
+            }
         }
     }
 }
@@ -2690,9 +2704,16 @@ Layout layout_for(const yrss_ctx *c, uint32_t n, uint32_t grid)
     // to flush and the scan to pass over, but a coarser deal of the batch to
     // the parse waves: 4 tiles up to 16 buckets (8 tiles cost the parse ~7 us
     // at 9 buckets), 8 tiles to 128 (the scan 9.8 -> 6.4 us at 65 buckets,
-    // r03 A/B; the bucket still packs beside a 9-bit rank), 16 beyond (the
-    // parse's count slots: 16 chunks a wave x nb <= kCntWords)
-    const uint64_t ct_nb = c->nb <= 16u ? 4u : c->nb <= 128u ? 8u : 16u;
+    // r03 A/B; the bucket still packs beside a 9-bit rank).  Past 128 buckets
+    // the rank sits beside q whatever the chunk, and two chunks a wave, up to
+    // 64 tiles, were fastest (256 buckets at 2^24 packets, 16 -> 32 -> 64
+    // tiles: step 0.3046 -> 0.3012 -> 0.2961 ms, scan 8.2 -> 5.0 -> 4.7 us,
+    // scatter 64 -> 62 -> 60 us; 128 tiles no better;
+    // profiles/r04_chunk32_grouped_ab.log, r04_chunk_sweep_{a,b}.log)
+    uint64_t ct_many = 16u;
+    while (ct_many < 64u && ct_many * 2u * 2u * waves <= tiles)
+        ct_many *= 2u;
+    const uint64_t ct_nb = c->nb <= 16u ? 4u : c->nb <= 128u ? 8u : ct_many;
     uint64_t ct = std::max<uint64_t>(c->tune.chunk_tiles ? c->tune.chunk_tiles : ct_nb,
                                      (tiles + max_chunks - 1) / max_chunks);
     uint32_t ct_shift = 0;
