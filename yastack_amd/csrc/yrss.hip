@@ -805,7 +805,10 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
 // with non-temporal stores alone the lines stayed dirty past the scatter and
 // their write-back landed in the next batch's parse kernel (+19 us there at 9
 // buckets, same-process A/B, profiles/r03_ab_inproc_store.log).
-constexpr int kListAux = 18;   // nt | sc1
+#ifndef YRSS_LIST_AUX   // A/B builds only
+#define YRSS_LIST_AUX 18
+#endif
+constexpr int kListAux = YRSS_LIST_AUX;   // nt | sc1
 
 // The lists as a buffer resource: offsets are 32-bit, so lists past 2^29
 // entries take flat non-temporal stores instead (wide = false).
