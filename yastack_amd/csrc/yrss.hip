@@ -53,7 +53,12 @@ constexpr int kScatterBlock = 256;     // 4 waves per scatter workgroup (halved 
 constexpr int kScatterWaves = kScatterBlock / kWave;
 constexpr uint32_t kMaxChunks = 65536;  // per launch; bounds the count matrix [nb][ncol]
 constexpr uint32_t kCntWords = 2176;    // parse: per-wave LDS count slots (chunks x nb): 32 x 68
-constexpr uint32_t kScanTile = 4096;    // scan: chunk columns per workgroup
+// scan: chunk columns per workgroup are up to kScanSub sub-tiles of 4096
+// (ScanParams.sub): two where the columns come in whole 8192s, so a 65-bucket
+// launch is 260 workgroups, resident at once, not 520 (scan 6.2 -> 5.3 us,
+// profiles/r04_scan_subtile_ab.log); the column count stays a multiple of 4096
+constexpr uint32_t kScanSub = 2;
+constexpr uint32_t kScanTile = 4096;
 constexpr uint32_t kPiece = 2048;       // fallback scatter: packets ranked and staged at once per wave
 constexpr uint32_t kPieceSlots = kPiece / 64;   // 64-packet slots of a piece
 // Toeplitz key tables: the 96 tuple bits are cut into 12 bytes (MSB first);
@@ -533,6 +538,10 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
     }
 }
 
+#ifndef YRSS_FLUSH_AUX   // A/B builds only
+#define YRSS_FLUSH_AUX 0      // plain
+#endif
+
 // ---------------------------------------------------------------------------
 // Kernel 1 entry.
 //   kCount   1: also count packets per bucket per chunk (per-queue lists on);
@@ -666,7 +675,13 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         // kBlock / kWaves, carried into (j, b) without a division.  The flush
         // costs ~5 us at 65 and 256 buckets, ~0 at 4 (a build without it,
         // profiles/r04_cntflush_ab.log).
+        // Plain stores: written through (nt | sc1) the counts made the scan
+        // reading them 1 us slower at 65 buckets, and the parse kernel was
+        // -6 us in one run and +3 us in another (profiles/r04_flush_policy_ab.log,
+        // r04_early_flush_ab.log)
         static_assert(kBlock % kWaves == 0, "a thread keeps its wave");
+        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+            P.seg_cnt, 0, (int)min((uint64_t)P.nb * P.ncol * 4u, (uint64_t)0x7fffffffu), kRsrcWord3);
         const uint32_t w = threadIdx.x % kWaves;
         uint32_t j = 0, b = threadIdx.x / kWaves;
         while (b >= P.nb) {
@@ -677,7 +692,9 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
             const uint32_t col = g0 + w + j * W;
 #ifndef YRSS_NO_CNT_FLUSH   // measurement builds only: the flush's cost (lists then wrong)
             if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords)
-                P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
+                __builtin_amdgcn_raw_buffer_store_b32(cnt_base[w * kCntWords + j * P.nb + b], rc,
+                                                      (int)(((size_t)b * P.ncol + col) * 4u), 0,
+                                                      YRSS_FLUSH_AUX);
 #endif
             b += kBlock / kWaves;
             while (b >= P.nb) {
@@ -702,6 +719,7 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
 // ---------------------------------------------------------------------------
 constexpr int kScanBlock = 1024;
 static_assert(kMaxChunks / kScanTile <= kWave, "one look-back lane per scan tile");
+static_assert(kScanBlock * 4 == 4096, "a sub-tile is one 16-byte word a thread");
 constexpr uint64_t kStFlagP = 1ull << 63;   // status holds the inclusive prefix
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, uint32_t lane)
@@ -727,6 +745,7 @@ struct ScanParams {
     unsigned long long *status;   // [nb][tiles]: flag | epoch:31 | value:32
     uint32_t *fault;
     uint32_t nchunk, ncol, tiles, epoch;
+    uint32_t sub;            // 4096-column sub-tiles a workgroup (1..kScanSub)
 };
 
 __device__ __forceinline__ unsigned long long scan_status(uint32_t epoch, bool incl, uint32_t v)
@@ -736,34 +755,49 @@ __device__ __forceinline__ unsigned long long scan_status(uint32_t epoch, bool i
 
 __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
 {
-    __shared__ uint32_t wsum[kScanBlock / kWave];
+    // kScanSub sub-tiles of 4096 columns, sub-tile k's 16-byte word t at
+    // column 4 (k 1024 + t): every load instruction reads 16 KB contiguous,
+    // and each sub-tile is its own block scan, offset by the earlier ones
+    __shared__ uint32_t wsum[kScanSub][kScanBlock / kWave];
+    __shared__ uint32_t sub_sh[kScanSub];
     __shared__ uint32_t prefix_sh;
     const uint32_t b = blockIdx.x / P.tiles, p = blockIdx.x % P.tiles;
     const uint32_t lane = lane_id(), wave = threadIdx.x / kWave;
-    const uint32_t col = p * kScanTile + threadIdx.x * 4u;
     const uint4 *row = reinterpret_cast<const uint4 *>(P.cnt + (size_t)b * P.ncol);
-    uint4 v = row[col / 4u];
-    // columns past the last chunk were never written this launch
-    if (col + 0u >= P.nchunk) v.x = 0;
-    if (col + 1u >= P.nchunk) v.y = 0;
-    if (col + 2u >= P.nchunk) v.z = 0;
-    if (col + 3u >= P.nchunk) v.w = 0;
-    const uint32_t local = v.x + v.y + v.z + v.w;
-    const uint32_t x = wave_incl_scan(local, lane);
-    if (lane == kWave - 1)
-        wsum[wave] = x;
+    uint4 v[kScanSub];
+    uint32_t local[kScanSub], x[kScanSub];
+#pragma unroll
+    for (uint32_t k = 0; k < kScanSub; ++k) {
+        const uint32_t col = (p * P.sub + k) * kScanTile + threadIdx.x * 4u;
+        v[k] = k < P.sub ? row[col / 4u] : uint4{0u, 0u, 0u, 0u};
+        // columns past the last chunk were never written this launch
+        if (col + 0u >= P.nchunk) v[k].x = 0;
+        if (col + 1u >= P.nchunk) v[k].y = 0;
+        if (col + 2u >= P.nchunk) v[k].z = 0;
+        if (col + 3u >= P.nchunk) v[k].w = 0;
+        local[k] = v[k].x + v[k].y + v[k].z + v[k].w;
+        x[k] = wave_incl_scan(local[k], lane);
+        if (lane == kWave - 1)
+            wsum[k][wave] = x[k];
+    }
     __syncthreads();
     if (wave == 0) {
-        const uint32_t w = lane < kScanBlock / kWave ? wsum[lane] : 0u;
-        const uint32_t ws = wave_incl_scan(w, lane);
-        if (lane < kScanBlock / kWave)
-            wsum[lane] = ws;
-        // Lane 15 holds the tile total: publish it, then sum every
-        // predecessor's aggregate at once (one lane per tile, <= 64 tiles per
-        // row), so no tile waits on a chain of inclusive prefixes.
+        uint32_t total = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kScanSub; ++k) {
+            const uint32_t w = lane < kScanBlock / kWave ? wsum[k][lane] : 0u;
+            const uint32_t ws = wave_incl_scan(w, lane);
+            if (lane < kScanBlock / kWave)
+                wsum[k][lane] = ws;
+            if (lane == 0)
+                sub_sh[k] = total;
+            total += __shfl(ws, kScanBlock / kWave - 1, kWave);
+        }
+        // publish the tile total, then sum every predecessor's aggregate at
+        // once (one lane per tile, <= 64 tiles per row), so no tile waits on
+        // a chain of inclusive prefixes
         unsigned long long *st = P.status + (size_t)b * P.tiles;
-        const uint32_t total = __shfl(ws, kScanBlock / kWave - 1, kWave);
-        if (lane == kScanBlock / kWave - 1)
+        if (lane == 0)
             __hip_atomic_store(&st[p], scan_status(P.epoch, false, total), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         uint32_t mine = 0, spins = 0;
@@ -792,13 +826,19 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
         }
     }
     __syncthreads();
-    uint32_t run = prefix_sh + x - local + (wave ? wsum[wave - 1] : 0u);
-    uint4 o;
-    o.x = run; run += v.x;
-    o.y = run; run += v.y;
-    o.z = run; run += v.z;
-    o.w = run;
-    reinterpret_cast<uint4 *>(P.off + (size_t)b * P.ncol)[col / 4u] = o;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanSub; ++k) {
+        if (k >= P.sub)
+            break;
+        const uint32_t col = (p * P.sub + k) * kScanTile + threadIdx.x * 4u;
+        uint32_t run = prefix_sh + sub_sh[k] + x[k] - local[k] + (wave ? wsum[k][wave - 1] : 0u);
+        uint4 o;
+        o.x = run; run += v[k].x;
+        o.y = run; run += v[k].y;
+        o.z = run; run += v[k].z;
+        o.w = run;
+        reinterpret_cast<uint4 *>(P.off + (size_t)b * P.ncol)[col / 4u] = o;
+    }
 }
 
 // List stores are streaming and written through at device scope (nt | sc1):
@@ -809,6 +849,20 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
 #define YRSS_LIST_AUX 18
 #endif
 constexpr int kListAux = YRSS_LIST_AUX;   // nt | sc1
+// Past 64 buckets the line scatter's stores are non-temporal only: its
+// scatter ran 1.5-2.3 us (65 buckets) and 2.3-3.9 us (256) faster and the next
+// batch's parse kernel no slower; at 9 buckets nt alone slowed the next parse
+// kernel (+19 us in round 3, +7 in round 4), so fewer buckets keep nt | sc1
+// (profiles/r04_list_policy_ab.log, r04_partial_quads_ab.log)
+#ifndef YRSS_LIST_AUX_MANY   // A/B builds only
+#define YRSS_LIST_AUX_MANY 2
+#endif
+constexpr int kListAuxMany = YRSS_LIST_AUX_MANY;
+constexpr uint32_t kListNtBuckets = 64;
+#ifndef YRSS_ONE_AUX   // A/B builds only
+#define YRSS_ONE_AUX 18
+#endif
+constexpr int kOneAux = YRSS_ONE_AUX;     // the one-list path's identity stores
 
 // The lists as a buffer resource: offsets are 32-bit, so lists past 2^29
 // entries take flat non-temporal stores instead (wide = false).
@@ -1195,6 +1249,8 @@ struct LineParams {
     uint32_t gshift, cshift;   // span = 2^gshift chunks, chunk = 2^cshift packets
     uint32_t lmax;             // stage lines: seg / 16 + 2 nb + 1
     uint32_t xcd;              // workgroups of one XCD take consecutive ranges
+    uint32_t nt;               // list stores non-temporal only (no sc1): past 64 buckets
+    uint32_t early;            // first span's loads before the totals: past 16 buckets
 };
 
 // LDS of a workgroup, in words: per-bucket arrays, the prefix table, the
@@ -1297,71 +1353,11 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // list position x is "adjusted" a = x + ph: 64-byte lines are a >> 4
     const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 15u);
 
-    // list starts (exclusive scan of totals); workgroup 0 also writes qstart.
-    // Every bucket block's total is loaded before the first is scanned: one
-    // round trip, not one per 64 buckets.
-    if (wave == 0) {
-        constexpr uint32_t kTB = kG == 2u ? 2u : 8u;   // nb <= 64 kTB
-        uint32_t tv[kTB];
-#pragma unroll
-        for (uint32_t i = 0; i < kTB; ++i) {
-            const uint32_t b = i * kWave + lane;
-            tv[i] = i * kWave < nb && b < nb ? P.totals[b] : 0u;
-        }
-        uint32_t carry = 0, nzb = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < kTB; ++i) {
-            if (i * kWave >= nb)   // (uniform)
-                break;
-            const uint32_t b = i * kWave + lane;
-            const uint32_t x0 = tv[i];
-            nzb += (uint32_t)__popcll(__ballot(x0 != 0u));
-            const uint32_t x = wave_incl_scan(x0, lane);
-            if (b < nb) {
-                start[b] = carry + x - x0;
-                if (blockIdx.x == 0)
-                    P.qstart[b] = carry + x - x0;
-            }
-            carry += __shfl(x, kWave - 1, kWave);
-        }
-        if (lane == 0) {
-            if (blockIdx.x == 0)
-                P.qstart[nb] = carry;
-            misc[0] = nzb;
-            misc[1] = 0u;
-            misc[3] = 0u;
-        }
-    }
-    __syncthreads();
-    if (misc[0] == 1u) {
-        // one non-empty list (all-UDP traffic): 0, 1, ..., n-1, grid-stride
-        // 16-byte non-temporal stores (64 MB in 10.7 us,
-        // profiles/r02_v8_hbm_write.log)
-        const ListOut lo = list_out(P.qidx, P.n);
-        const uint32_t ph4 = ph & 3u;
-        const uint32_t head = min(P.n, (4u - ph4) & 3u);
-        const uint32_t nv = (P.n - head) >> 2;
-        const uint32_t T = gridDim.x * blockDim.x;
-        const uint32_t id = blockIdx.x * blockDim.x + t;
-        if (id < head)
-            list_store1<kListAux>(lo, id, id);
-        for (uint32_t v = id; v < nv; v += T) {
-            const uint32_t x = head + 4u * v;
-            list_store4<kListAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
-        }
-        const uint32_t e = head + 4u * nv + id;
-        if (e < P.n)
-            list_store1<kListAux>(lo, e, e);
-        return;
-    }
-
     // this workgroup's range of spans
     const uint32_t nsp = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
     const uint32_t r = xcd_block(P.xcd), G = gridDim.x;
     const uint32_t g0 = (uint32_t)((uint64_t)r * nsp / G);
     const uint32_t g1 = (uint32_t)((uint64_t)(r + 1u) * nsp / G);
-    if (g0 >= g1)
-        return;
     // prefix table rows are ncs + 1 words apart: with a power-of-two row the
     // lanes of one chunk column hit one or two LDS banks whatever their bucket
     // (a 0.78 conflict share of the LDS cycles at 64 buckets)
@@ -1376,7 +1372,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // set 1 holds the state before the range's first span (set 0): its
     // prefixes are loaded beside the first span's streams (one round trip for
     // both) and written once they have arrived
-    const uint32_t pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
+    uint32_t pre0 = 0;
     const ListOut lout = list_out(P.qidx, P.n);
     // The span's streams alternate between two register sets: span g+1's
     // loads issue at the start of span g's phase (b), once its table is in
@@ -1437,7 +1433,77 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo,
                                                              (int)(c0 * 4u + k * step), 0);
     };
-    load_span(g0, pkA, qkA);
+    // Past 16 buckets the first span's streams and prefixes are issued before
+    // the totals are read, so the two round trips overlap (such batches are
+    // rarely one-list, where these loads go unused)
+    if (P.early && g0 < g1) {
+        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
+        load_span(g0, pkA, qkA);
+    }
+    // list starts (exclusive scan of totals); workgroup 0 also writes qstart.
+    // Every bucket block's total is loaded before the first is scanned: one
+    // round trip, not one per 64 buckets.
+    if (wave == 0) {
+        constexpr uint32_t kTB = kG == 2u ? 2u : 8u;   // nb <= 64 kTB
+        uint32_t tv[kTB];
+#pragma unroll
+        for (uint32_t i = 0; i < kTB; ++i) {
+            const uint32_t b = i * kWave + lane;
+            tv[i] = i * kWave < nb && b < nb ? P.totals[b] : 0u;
+        }
+        uint32_t carry = 0, nzb = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kTB; ++i) {
+            if (i * kWave >= nb)   // (uniform)
+                break;
+            const uint32_t b = i * kWave + lane;
+            const uint32_t x0 = tv[i];
+            nzb += (uint32_t)__popcll(__ballot(x0 != 0u));
+            const uint32_t x = wave_incl_scan(x0, lane);
+            if (b < nb) {
+                start[b] = carry + x - x0;
+                if (blockIdx.x == 0)
+                    P.qstart[b] = carry + x - x0;
+            }
+            carry += __shfl(x, kWave - 1, kWave);
+        }
+        if (lane == 0) {
+            if (blockIdx.x == 0)
+                P.qstart[nb] = carry;
+            misc[0] = nzb;
+            misc[1] = 0u;
+            misc[3] = 0u;
+        }
+    }
+    __syncthreads();
+    if (misc[0] == 1u) {
+        // one non-empty list (all-UDP traffic): 0, 1, ..., n-1, grid-stride
+        // 16-byte non-temporal stores (64 MB in 10.7 us,
+        // profiles/r02_v8_hbm_write.log)
+        const ListOut lo = list_out(P.qidx, P.n);
+        const uint32_t ph4 = ph & 3u;
+        const uint32_t head = min(P.n, (4u - ph4) & 3u);
+        const uint32_t nv = (P.n - head) >> 2;
+        const uint32_t T = gridDim.x * blockDim.x;
+        const uint32_t id = blockIdx.x * blockDim.x + t;
+        if (id < head)
+            list_store1<kOneAux>(lo, id, id);
+        for (uint32_t v = id; v < nv; v += T) {
+            const uint32_t x = head + 4u * v;
+            list_store4<kOneAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
+        }
+        const uint32_t e = head + 4u * nv + id;
+        if (e < P.n)
+            list_store1<kOneAux>(lo, e, e);
+        return;
+    }
+
+    if (g0 >= g1)
+        return;
+    if (!P.early) {
+        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
+        load_span(g0, pkA, qkA);
+    }
     // the first span's loads waited for here, so that at the loop head no
     // load is pending on any path: a pending one there made the compiler wait
     // vmcnt(0) at the prefix table's first use in every span, i.e. for the
@@ -1614,7 +1680,10 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             if (mode == 0u) {
                 const uint32_t d = a0 - ph;
                 if (d + 4u <= P.n && d + 4u > d) {
-                    list_store4<kListAux>(lout, d, e);
+                    if (P.nt)
+                        list_store4<kListAuxMany>(lout, d, e);
+                    else
+                        list_store4<kListAux>(lout, d, e);
                     wrote += 4u;
                     wsum += e.x + e.y + e.z + e.w;
                 } else {
@@ -1622,6 +1691,25 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 }
             } else if (mode == 2u) {
                 const uint32_t b = tag & 0xffffu, v0 = cs[b], e1 = ve[b];
+                // a partial line (a range's first or last line of a bucket):
+                // its quads inside [v0, e1) still leave as one 16-byte store,
+                // only the quad the bounds cut goes word by word (word stores
+                // for every quad of such lines tripled the scatter's store
+                // instructions at 256 buckets)
+                if (a0 >= v0 && a0 + 4u <= e1) {
+                    const uint32_t d = a0 - ph;
+                    if (d + 4u <= P.n && d + 4u > d) {
+                        if (P.nt)
+                            list_store4<kListAuxMany>(lout, d, e);
+                        else
+                            list_store4<kListAux>(lout, d, e);
+                        wrote += 4u;
+                        wsum += e.x + e.y + e.z + e.w;
+                    } else {
+                        report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
+                    }
+                    return;
+                }
 #pragma unroll
                 for (uint32_t j = 0; j < 4u; ++j) {
                     const uint32_t a = a0 + j;
@@ -1629,7 +1717,10 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                         continue;
                     const uint32_t w = e[j], d = a - ph;
                     if (d < P.n) {
-                        list_store1<kListAux>(lout, d, w);
+                        if (P.nt)
+                            list_store1<kListAuxMany>(lout, d, w);
+                        else
+                            list_store1<kListAux>(lout, d, w);
                         ++wrote;
                         wsum += w;
                     } else {
@@ -3614,7 +3705,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         SP.fault = c->d_fault_rec;
         SP.nchunk = lay.nchunk;
         SP.ncol = lay.ncol;
-        SP.tiles = lay.ncol / kScanTile;
+        SP.sub = lay.ncol % (kScanSub * kScanTile) == 0 ? kScanSub : 1u;
+        SP.tiles = lay.ncol / (kScanTile * SP.sub);
         if ((++W.scan_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
             ++W.scan_epoch;
         SP.epoch = W.scan_epoch;
@@ -3641,6 +3733,11 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         S.cshift = lay.ct_shift + 6u;
         S.lmax = lp.lmax;
         S.xcd = c->tune.scatter_xcd != 0 ? 1u : 0u;
+        S.nt = c->nb > kListNtBuckets ? 1u : 0u;
+#ifndef YRSS_EARLY_NB   // A/B builds only
+#define YRSS_EARLY_NB 16
+#endif
+        S.early = c->nb > YRSS_EARLY_NB ? 1u : 0u;
         // persistent: the resident workgroups, each one contiguous range of
         // spans, never more workgroups than spans
         const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
