@@ -1692,10 +1692,10 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             } else if (mode == 2u) {
                 const uint32_t b = tag & 0xffffu, v0 = cs[b], e1 = ve[b];
                 // a partial line (a range's first or last line of a bucket):
-                // its quads inside [v0, e1) still leave as one 16-byte store,
-                // only the quad the bounds cut goes word by word (word stores
-                // for every quad of such lines tripled the scatter's store
-                // instructions at 256 buckets)
+                // its quads inside [v0, e1) still leave as one 16-byte store;
+                // a quad the bounds cut is left to the cut pass below (word
+                // stores for every quad of such lines tripled the scatter's
+                // store instructions at 256 buckets)
                 if (a0 >= v0 && a0 + 4u <= e1) {
                     const uint32_t d = a0 - ph;
                     if (d + 4u <= P.n && d + 4u > d) {
@@ -1709,23 +1709,6 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                         report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
                     }
                     return;
-                }
-#pragma unroll
-                for (uint32_t j = 0; j < 4u; ++j) {
-                    const uint32_t a = a0 + j;
-                    if (a < v0 || a >= e1)
-                        continue;
-                    const uint32_t w = e[j], d = a - ph;
-                    if (d < P.n) {
-                        if (P.nt)
-                            list_store1<kListAuxMany>(lout, d, w);
-                        else
-                            list_store1<kListAux>(lout, d, w);
-                        ++wrote;
-                        wsum += w;
-                    } else {
-                        report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
-                    }
                 }
             }
         };
@@ -1756,6 +1739,37 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
 #pragma unroll
             for (uint32_t i = 0; i < kCopyQ; ++i)
                 copy_quad(v0 + i * nct, tg[i], gl[i], eq[i]);
+        }
+        // The cut quads of partial lines: per bucket at most two, the quad
+        // holding its first valid position cs (when unaligned) and the one
+        // holding its end ve (when unaligned and the line leaves now, i.e.
+        // the range ends here).  A thread per (bucket, quad, word), one word
+        // a lane, from the stage: a wave-instruction stores 64 such words
+        // where the copy-out's per-quad word stores cost four
+        // wave-instructions for every turn that held one
+        for (uint32_t e = t; e < 8u * nb; e += kLineBlock) {
+            const uint32_t b = e >> 3, k = (e >> 2) & 1u, j = e & 3u;
+            const uint32_t v0 = cs[b], e1 = ve[b];
+            const uint32_t qb = (k ? e1 : v0) & ~3u, a = qb + j;
+            bool go = a >= v0 && a < e1 && ((k ? e1 : v0) & 3u) != 0u;
+            if (k == 0u)   // the first cut quad's line leaves now unless carried
+                go = go && !(!last && (v0 >> 4) == (e1 >> 4) && (e1 & 15u) != 0u);
+            else           // the end's line leaves now only at the range's end;
+                           // a quad holding both bounds, v0 unaligned, is k = 0's
+                go = go && last && !(qb == (v0 & ~3u) && (v0 & 3u) != 0u);
+            if (go) {
+                const uint32_t w = stg[min(so[b] + a, cap)], d = a - ph;
+                if (d < P.n) {
+                    if (P.nt)
+                        list_store1<kListAuxMany>(lout, d, w);
+                    else
+                        list_store1<kListAux>(lout, d, w);
+                    ++wrote;
+                    wsum += w;
+                } else {
+                    report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
+                }
+            }
         }
         LPROF(4);
         // (d) carry the unfinished last lines
