@@ -538,10 +538,6 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
     }
 }
 
-#ifndef YRSS_FLUSH_AUX   // A/B builds only
-#define YRSS_FLUSH_AUX 0      // plain
-#endif
-
 // ---------------------------------------------------------------------------
 // Kernel 1 entry.
 //   kCount   1: also count packets per bucket per chunk (per-queue lists on);
@@ -680,8 +676,6 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         // -6 us in one run and +3 us in another (profiles/r04_flush_policy_ab.log,
         // r04_early_flush_ab.log)
         static_assert(kBlock % kWaves == 0, "a thread keeps its wave");
-        const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-            P.seg_cnt, 0, (int)min((uint64_t)P.nb * P.ncol * 4u, (uint64_t)0x7fffffffu), kRsrcWord3);
         const uint32_t w = threadIdx.x % kWaves;
         uint32_t j = 0, b = threadIdx.x / kWaves;
         while (b >= P.nb) {
@@ -692,9 +686,7 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
             const uint32_t col = g0 + w + j * W;
 #ifndef YRSS_NO_CNT_FLUSH   // measurement builds only: the flush's cost (lists then wrong)
             if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords)
-                __builtin_amdgcn_raw_buffer_store_b32(cnt_base[w * kCntWords + j * P.nb + b], rc,
-                                                      (int)(((size_t)b * P.ncol + col) * 4u), 0,
-                                                      YRSS_FLUSH_AUX);
+                P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
 #endif
             b += kBlock / kWaves;
             while (b >= P.nb) {
@@ -845,24 +837,14 @@ __global__ __launch_bounds__(kScanBlock) void yrss_seg_scan(ScanParams P)
 // with non-temporal stores alone the lines stayed dirty past the scatter and
 // their write-back landed in the next batch's parse kernel (+19 us there at 9
 // buckets, same-process A/B, profiles/r03_ab_inproc_store.log).
-#ifndef YRSS_LIST_AUX   // A/B builds only
-#define YRSS_LIST_AUX 18
-#endif
-constexpr int kListAux = YRSS_LIST_AUX;   // nt | sc1
+constexpr int kListAux = 18;   // nt | sc1
 // Past 64 buckets the line scatter's stores are non-temporal only: its
 // scatter ran 1.5-2.3 us (65 buckets) and 2.3-3.9 us (256) faster and the next
 // batch's parse kernel no slower; at 9 buckets nt alone slowed the next parse
 // kernel (+19 us in round 3, +7 in round 4), so fewer buckets keep nt | sc1
 // (profiles/r04_list_policy_ab.log, r04_partial_quads_ab.log)
-#ifndef YRSS_LIST_AUX_MANY   // A/B builds only
-#define YRSS_LIST_AUX_MANY 2
-#endif
-constexpr int kListAuxMany = YRSS_LIST_AUX_MANY;
+constexpr int kListAuxMany = 2;   // nt
 constexpr uint32_t kListNtBuckets = 64;
-#ifndef YRSS_ONE_AUX   // A/B builds only
-#define YRSS_ONE_AUX 18
-#endif
-constexpr int kOneAux = YRSS_ONE_AUX;     // the one-list path's identity stores
 
 // The lists as a buffer resource: offsets are 32-bit, so lists past 2^29
 // entries take flat non-temporal stores instead (wide = false).
@@ -1487,14 +1469,14 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         const uint32_t T = gridDim.x * blockDim.x;
         const uint32_t id = blockIdx.x * blockDim.x + t;
         if (id < head)
-            list_store1<kOneAux>(lo, id, id);
+            list_store1<kListAux>(lo, id, id);
         for (uint32_t v = id; v < nv; v += T) {
             const uint32_t x = head + 4u * v;
-            list_store4<kOneAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
+            list_store4<kListAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
         }
         const uint32_t e = head + 4u * nv + id;
         if (e < P.n)
-            list_store1<kOneAux>(lo, e, e);
+            list_store1<kListAux>(lo, e, e);
         return;
     }
 
@@ -3748,10 +3730,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         S.lmax = lp.lmax;
         S.xcd = c->tune.scatter_xcd != 0 ? 1u : 0u;
         S.nt = c->nb > kListNtBuckets ? 1u : 0u;
-#ifndef YRSS_EARLY_NB   // A/B builds only
-#define YRSS_EARLY_NB 16
-#endif
-        S.early = c->nb > YRSS_EARLY_NB ? 1u : 0u;
+        S.early = c->nb > 16u ? 1u : 0u;
         // persistent: the resident workgroups, each one contiguous range of
         // spans, never more workgroups than spans
         const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
