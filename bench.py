@@ -80,6 +80,10 @@ def parse_args(argv=None):
     ap.add_argument("--tune", default="",
                     help="layout overrides for measurements, k=v[,k=v] (yrss_set_tuning "
                          "fields: chunk_tiles, span_tiles, parse_blocks, scatter_xcd)")
+    ap.add_argument("--extra-configs", default="vlan6_tcp,jumbo_tcp4",
+                    help="after the headline, each rank also classifies a --pkts shard of "
+                         "these profiles (BASELINE configs[3], configs[4]: the 8-GPU "
+                         "configs), reported under configs_extra, never as value ('' = off)")
     ap.add_argument("--dry", action="store_true",
                     help="plumbing check without a GPU (rank spawn, barrier, reductions); "
                          "prints a line marked dry, never a measurement")
@@ -207,16 +211,19 @@ def sum_over_ranks(x: float, world: int) -> float:
 CPU_PROFILES = ("udp4", "tcp4")        # the headline stream, and every packet hashed
 CPU_VARIANTS = ("bit_serial", "table")  # toeplitz_hash as written; 12x256 byte tables
 CPU_RUNS = 3                            # timed windows per cell: median, min, max
+OVERLAP_MIN = 0.95                      # a multi-process cell below this is flagged
 
 
 def cpu_worker(spec: str) -> int:
-    """One pinned CPU-baseline process (bench.py --cpu-worker prof:variant:secs:cpu):
+    """One pinned CPU-baseline process (bench.py --cpu-worker prof:variant:cpu):
     the oracle's toeplitz_dispatch restatement over 2^20 packets of the stream,
-    one call per packet, repeated for about `secs` per timed window.  Every
-    "go" line on stdin starts one window; the answer carries the window's
-    CLOCK_MONOTONIC start and end, so the parent can check that the windows of
-    a cell's processes overlapped."""
-    prof, variant, secs, cpu = spec.split(":")
+    one call per packet, inlined or (variant suffix "_fnptr") through the
+    registered-dispatcher function pointer as process_packets calls it
+    (ff_dpdk_if.c:1078-1079).  Every "go START END" line on stdin runs one
+    window between those CLOCK_MONOTONIC instants (ns), so all processes of a
+    cell run over the same stretch of time; the answer carries the packets and
+    the window's actual first and last instants."""
+    prof, variant, cpu = spec.split(":")
     if cpu != "-":
         os.sched_setaffinity(0, {int(cpu)})     # what taskset -c does
     from oracle import oracle
@@ -224,29 +231,33 @@ def cpu_worker(spec: str) -> int:
     n = 1 << 20
     win, lens = oracle.synth(PROFILES[prof], n, 0, SEED, NFLOWS[prof], 64)
     c = oracle.cfg(3, 3, 1, 1)                  # fs/config/config.ini knobs
-    fast = variant == "table"
-    t0 = time.perf_counter()
-    oracle.bench_dispatch(win, 64, lens, c, 1, fast)
-    reps = max(1, int(float(secs) / max(time.perf_counter() - t0, 1e-6)))
+    fast = variant.startswith("table")
+    fnptr = variant.endswith("_fnptr")
+    t = time.monotonic_ns()
+    oracle.bench_window(win, 64, lens, c, fast, fnptr, t, t + 20_000_000)   # warm caches
     print("ready", flush=True)
-    while sys.stdin.readline().strip() == "go":
-        t0 = time.monotonic()
-        oracle.bench_dispatch(win, 64, lens, c, reps, fast)
-        t1 = time.monotonic()
-        print(json.dumps({"pkts": reps * n, "t0": t0, "t1": t1}), flush=True)
+    for line in sys.stdin:
+        parts = line.split()
+        if not parts or parts[0] != "go":
+            break
+        pkts, t0, t1 = oracle.bench_window(win, 64, lens, c, fast, fnptr, int(parts[1]),
+                                           int(parts[2]))
+        print(json.dumps({"pkts": pkts, "t0": t0 / 1e9, "t1": t1 / 1e9}), flush=True)
     return 0
 
 
 def _cpu_run(prof: str, variant: str, secs: float, cpus, runs: int = CPU_RUNS):
-    """len(cpus) pinned worker processes, started once and released together
-    for `runs` windows.  A window's rate is the sum of the processes' own rates;
+    """len(cpus) pinned worker processes, started once and given `runs`
+    common windows [start, start + secs] on CLOCK_MONOTONIC.  A window's rate
+    is the sum of the processes' own rates, each over its own actual stretch;
     `overlap` is the shortest common stretch of a window over its longest
-    process (1.0 = they ran side by side the whole time)."""
+    process (1.0 = side by side the whole time; below OVERLAP_MIN the cell is
+    flagged, its rate is then not a simultaneous one)."""
     import subprocess
     import statistics
 
     procs = [subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--cpu-worker",
-                               f"{prof}:{variant}:{secs}:{cpu}"],
+                               f"{prof}:{variant}:{cpu}"],
                               stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
              for cpu in cpus]
     rates, overlaps = [], []
@@ -255,8 +266,10 @@ def _cpu_run(prof: str, variant: str, secs: float, cpus, runs: int = CPU_RUNS):
             if p.stdout.readline().strip() != "ready":
                 raise RuntimeError("cpu worker failed to start")
         for _ in range(runs):
+            start = time.monotonic_ns() + 50_000_000    # every process is waiting by then
+            end = start + int(secs * 1e9)
             for p in procs:
-                p.stdin.write("go\n")
+                p.stdin.write(f"go {start} {end}\n")
                 p.stdin.flush()
             res = [json.loads(p.stdout.readline()) for p in procs]
             rates.append(sum(r["pkts"] / (r["t1"] - r["t0"]) for r in res) / 1e6)
@@ -268,9 +281,12 @@ def _cpu_run(prof: str, variant: str, secs: float, cpus, runs: int = CPU_RUNS):
     finally:
         for p in procs:
             p.wait(timeout=600)
-    return {"mpps": round(statistics.median(rates), 2), "min": round(min(rates), 2),
-            "max": round(max(rates), 2), "runs": len(rates),
-            "overlap": round(min(overlaps), 3)}
+    out = {"mpps": round(statistics.median(rates), 2), "min": round(min(rates), 2),
+           "max": round(max(rates), 2), "runs": len(rates),
+           "overlap": round(min(overlaps), 4)}
+    if len(cpus) > 1 and out["overlap"] < OVERLAP_MIN:
+        out["flag"] = f"overlap {out['overlap']} < {OVERLAP_MIN}: not a simultaneous rate"
+    return out
 
 
 def cpu_quota():
@@ -317,9 +333,12 @@ def cpu_baseline(args, nb_queues):
     reference's single dispatching lcore, ff_dpdk_if.c:1653) and on one GPU's
     share of the box (16 cores), as independent processes pinned one per
     physical core; and on every core the job's CPU quota lets it keep busy
-    (cgroup cpu.max, stated), SURVEY §8(d).  Every cell is the median of
-    CPU_RUNS timed windows with its min and max.  `value` is the bit-serial
-    port on 1 core over the bench's own stream."""
+    (cgroup cpu.max, stated), SURVEY §8(d).  The 1-core cells also run through
+    the registered-dispatcher function pointer (`_fnptr`), the call form of
+    process_packets (ff_dpdk_if.c:1078-1079).  Every cell is the median of
+    CPU_RUNS common timed windows with its min and max.  `value` is the
+    bit-serial port on 1 core over the bench's own stream, called through the
+    function pointer as the reference calls it; `value_inlined` beside it."""
     allowed = sorted(os.sched_getaffinity(0))
     phys = physical_cores(allowed) or allowed
     quota, qsrc = cpu_quota()
@@ -327,8 +346,8 @@ def cpu_baseline(args, nb_queues):
     share = phys[:share_n]                          # one GPU's share of the box's cores
     cells = [phys[:1], share]
     profs = list(dict.fromkeys([args.profile, *CPU_PROFILES]))   # the bench's own stream first
-    secs = max(0.3, args.cpu_seconds / ((len(cells) * len(profs) * len(CPU_VARIANTS) + 1) *
-                                        CPU_RUNS))
+    n_cells = len(profs) * (len(cells) * len(CPU_VARIANTS) + len(CPU_VARIANTS)) + 1
+    secs = max(0.3, args.cpu_seconds / (n_cells * CPU_RUNS))
     by = {}
     for prof in profs:
         by[prof] = {}
@@ -339,6 +358,10 @@ def cpu_baseline(args, nb_queues):
                 by[prof][var][str(len(cs))] = cell
                 print(f"cpu_baseline {prof} {var} {len(cs)} cores: {cell}", file=sys.stderr,
                       flush=True)
+            # the reference's call form: through dispatch_func_t, one core
+            cell = _cpu_run(prof, var + "_fnptr", secs, phys[:1])
+            by[prof][var + "_fnptr"] = {"1": cell}
+            print(f"cpu_baseline {prof} {var}_fnptr 1 core: {cell}", file=sys.stderr, flush=True)
     # every core the quota lets the job keep busy: the headline cell only
     all_cpus = (phys + [c for c in allowed if c not in set(phys)])[:quota]
     if quota > share_n:
@@ -356,6 +379,8 @@ def cpu_baseline(args, nb_queues):
     if all_cell["mpps"] < share_cell["mpps"]:
         all_note += (f"; below the {share_n}-core cell: the extra processes share cores "
                      "(SMT siblings or an over-committed quota)")
+    flagged = [f"{p}/{v}/{k}" for p, vs in by.items() for v, ks in vs.items()
+               for k, cell in ks.items() if "flag" in cell]
     cpu = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -365,20 +390,29 @@ def cpu_baseline(args, nb_queues):
     except OSError:
         pass
     head = args.profile
-    one = by[head]["bit_serial"]["1"]
+    one = by[head]["bit_serial_fnptr"]["1"]
+    inl = by[head]["bit_serial"]["1"]
     return {
         "value": one["mpps"], "unit": "Mpkt/s", "cores": 1, "kind": "port",
         "min": one["min"], "max": one["max"], "runs": one["runs"],
-        "sample": f"2^20 packets of each stream re-run for ~{secs:.2f}s per timed window, "
-                  f"median of {CPU_RUNS} windows per cell, one toeplitz_dispatch call per "
-                  "packet (oracle restatement, gcc -O2 fs/lib flags), processes pinned one "
-                  f"per physical core; host CPU: {cpu}; {len(allowed)} CPUs in the affinity "
+        "call": "through the registered dispatcher's function pointer (process_packets, "
+                "ff_dpdk_if.c:1078-1079)",
+        "value_inlined": inl["mpps"],
+        "sample": f"2^20 packets of each stream re-run over common windows of ~{secs:.2f}s "
+                  f"(CLOCK_MONOTONIC start and end shared by every process of a cell), median "
+                  f"of {CPU_RUNS} windows per cell, one toeplitz_dispatch call per packet "
+                  "(oracle restatement, gcc -O2 fs/lib flags), processes pinned one per "
+                  f"physical core; host CPU: {cpu}; {len(allowed)} CPUs in the affinity "
                   f"mask, quota {quota} ({qsrc})",
         "per_gpu_share": {"value": share_cell["mpps"], "min": share_cell["min"],
-                          "max": share_cell["max"], "unit": "Mpkt/s", "cores": share_n,
+                          "max": share_cell["max"], "overlap": share_cell["overlap"],
+                          "unit": "Mpkt/s", "cores": share_n,
                           "note": "the 16 host cores one GPU of the box is given"},
         "all_cores": {"value": all_cell["mpps"], "min": all_cell["min"], "max": all_cell["max"],
+                      "overlap": all_cell["overlap"],
                       "unit": "Mpkt/s", "cores": max(quota, share_n), "note": all_note},
+        "overlap_min": OVERLAP_MIN,
+        "flagged_cells": flagged,
         "by_profile": by,
     }
 
@@ -423,14 +457,24 @@ def _cpulist(text: str):
     return out
 
 
+def _siblings(cpu: int):
+    try:
+        return _cpulist(Path(f"/sys/devices/system/cpu/cpu{cpu}/topology/"
+                             "thread_siblings_list").read_text())
+    except (OSError, ValueError):
+        return [cpu]
+
+
 def gpu_placement(device: str):
     """NUMA node of the GPU (PCI address from device_identity) and the CPU the
-    host-resident dispatcher thread is pinned to: a CPU of that node this
-    process may run on, from the middle of the node's list rather than its
-    first (CPU 0 takes the box's housekeeping: the windows form's copy ran at
-    1256-1440 cycles a burst there, profiles/r04_final_bench.log); the
-    reference's dispatching lcore sits beside its NIC and GPU.  None where
-    sysfs does not say."""
+    host-resident dispatcher thread is pinned to: a physical core of that node
+    (the first SMT sibling of its core), from the middle of the node's cores,
+    never the node's first core nor that core's SMT twin (CPU 0 takes the box's
+    housekeeping: the windows form's copy ran at 1256-1440 cycles a burst
+    there, profiles/r04_final_bench.log; round 4's "middle of the node's CPU
+    list" landed on CPU 128 / 192, the SMT twins of the nodes' first cores,
+    VERDICT r04 weak 5).  The reference's dispatching lcore sits beside its
+    NIC and GPU.  None where sysfs does not say."""
     node, cpu = None, None
     try:
         node = int(Path(f"/sys/bus/pci/devices/{device}.0/numa_node").read_text())
@@ -441,10 +485,14 @@ def gpu_placement(device: str):
         try:
             local = _cpulist(Path(f"/sys/devices/system/node/node{node}/cpulist").read_text())
             mine = [c for c in local if c in set(allowed)]
-            cpu = mine[len(mine) // 2] if mine else None
+            first = set(_siblings(local[0])) if local else set()
+            cores = [c for c in physical_cores(mine) if c not in first]
+            cpu = cores[len(cores) // 2] if cores else (mine[len(mine) // 2] if mine else None)
         except (OSError, ValueError):
             cpu = None
-    return {"gpu_node": node, "dispatch_cpu": cpu}
+    sib = _siblings(cpu) if cpu is not None else []
+    return {"gpu_node": node, "dispatch_cpu": cpu, "dispatch_cpu_siblings": sib,
+            "dispatch_cpu_is_first_sibling": bool(sib) and cpu == min(sib)}
 
 
 def _cbench_rows(lines, keys):
@@ -531,7 +579,11 @@ def pcie_inclusive(profile: str, place=None):
             gbs = row["mpps"] * 1e6 * (rd + 10) / 1e9
             row.update({"link_bytes_per_pkt": rd + 10, "link_GBps": round(gbs, 2),
                         "link_frac": round(gbs / PCIE_GEN5_X16_GBS, 4),
-                        "gpu_node": place.get("gpu_node")})
+                        "gpu_node": place.get("gpu_node"),
+                        "dispatch_cpu": place.get("dispatch_cpu"),
+                        "dispatch_cpu_siblings": place.get("dispatch_cpu_siblings"),
+                        "dispatch_cpu_is_first_sibling":
+                            place.get("dispatch_cpu_is_first_sibling")})
             out.append(row)
     return out or None
 
@@ -572,6 +624,8 @@ def pcie_fanout(profile: str, world: int, place=None):
                 continue
         for row in _cbench_rows(lines, ("api", "burst", "gpus", "inflight", "blocks")):
             row["gpu_node"] = place.get("gpu_node")
+            row["dispatch_cpu"] = place.get("dispatch_cpu")
+            row["dispatch_cpu_is_first_sibling"] = place.get("dispatch_cpu_is_first_sibling")
             out.append(row)
     return out or None
 
@@ -657,6 +711,81 @@ def dry_run(args, world, rank, local):
 
         dist.destroy_process_group()
     return 0
+
+
+EXTRA_LABELS = {"vlan6_tcp": "configs[3]", "jumbo_tcp4": "configs[4]", "imix": "configs[2]",
+                "udp4": "configs[1]"}
+
+
+def run_extra_config(eng, profile, args, world, rank, devices):
+    """One more BASELINE config after the headline: each rank classifies its own
+    --pkts shard of `profile` (weak scaling, no collective on the data path),
+    timed like the headline (barrier + synchronize on both sides, max over
+    ranks) over min(steps, 20) steps of two rotated batches; the parse kernel
+    timed by events on its own dispatch packet; then checked against the oracle
+    (q and hash of the first --check packets, the whole per-queue lists)."""
+    import numpy as np
+    import torch
+
+    from oracle import oracle
+    from yastack_amd import abi
+
+    n = args.pkts
+    nbq = args.nb_queues or args.nb_procs
+    bats = []
+    for k in range(2):
+        w_k, l_k = eng.synth(PROFILES[profile], n, (rank * 2 + k) * n, SEED, NFLOWS[profile],
+                             args.stride)
+        bats.append((w_k, l_k, eng.alloc_out(n, w_k.device)))
+    it = [0]
+
+    def step():
+        w_k, l_k, o_k = bats[it[0] % 2]
+        it[0] += 1
+        eng.dispatch_dev(w_k, l_k, args.stride, n, out=o_k)
+
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    steps = max(1, min(args.steps, 20))
+    eng.timing_enable(1 << abi.K_PARSE_HASH)
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(world)
+    elapsed = max_over_ranks(t1 - t0, world)
+    k_ms, k_cnt = eng.timing_read(abi.K_PARSE_HASH)
+    eng.timing_enable(0)
+    k_s = max_over_ranks(k_ms / max(k_cnt, 1) / 1e3, world)
+    # the check, on the batch the last step classified
+    w_k, l_k, o_k = bats[(it[0] - 1) % 2]
+    m = min(args.check or (1 << 20), n)
+    c = oracle.cfg(args.nb_procs, nbq, 1, args.dispatch_only_core)
+    q_ref, h_ref = oracle.dispatch_windows(w_k[: m * args.stride].cpu().numpy(), args.stride,
+                                           l_k[:m].cpu().numpy().view(np.uint16), c)
+    ok = bool(np.array_equal(o_k.q[:m].cpu().numpy(), q_ref) and
+              np.array_equal(o_k.hash[:m].cpu().numpy().view(np.uint32), h_ref))
+    qi_ref, qs_ref = oracle.process_burst(o_k.q[:n].cpu().numpy(), nbq)
+    ok = ok and bool(np.array_equal(o_k.qstart.cpu().numpy().view(np.uint32), qs_ref) and
+                     np.array_equal(o_k.qidx[:n].cpu().numpy().view(np.uint32), qi_ref))
+    chk = reduce_check({"rank": rank, "device": devices[rank], "pkts_checked": m,
+                        "bit_exact": ok}, world)
+    del bats
+    total = sum_over_ranks(float(n * steps), world)
+    bpp = min(args.stride, 64) + 2 + 4 + 2
+    return {"config": EXTRA_LABELS.get(profile, profile), "profile": profile,
+            "workload": WORKLOADS[profile], "nflows": NFLOWS[profile], "n_gpus": world,
+            "pkts_per_gpu": n, "steps": steps,
+            "value": round(total / elapsed / 1e6, 2), "unit": "Mpkt/s",
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
+            "parse_us": round(k_s * 1e6, 2),
+            "roofline_frac": round(bpp * n / k_s / 1e9 / HBM_PEAK_GBS, 4) if k_s else None,
+            "ranks_checked": chk["ranks_checked"], "bit_exact": chk["bit_exact"],
+            "pkts_checked": chk["pkts_checked"]}
 
 
 def main(argv=None):
@@ -786,6 +915,18 @@ def main(argv=None):
                  "parse_us": round(k_ms / max(k_cnt, 1) * 1e3, 2)}
     check = reduce_check(check, world)
 
+    # the 8-GPU configs (and any other asked for), each rank its own shard,
+    # after the headline: a line for configs[3] / configs[4] at every N
+    extra = None
+    if args.extra_configs and not args.no_compact and not args.filter:
+        del batches, win, lens, out
+        torch.cuda.empty_cache()
+        extra = []
+        for p in [x for x in args.extra_configs.split(",") if x]:
+            extra.append(run_extra_config(eng, p, args, world, rank, devices))
+            if rank == 0:
+                print(f"configs_extra: {extra[-1]}", file=sys.stderr, flush=True)
+
     # the CPU baseline on rank 0 once every rank's device work is done (at any
     # N: the other ranks wait at the barrier)
     barrier(world)
@@ -846,6 +987,7 @@ def main(argv=None):
                     "reads_only_achieved": round((bpp - 6) * n / probe_rd_s / 1e9, 1)
                     if probe_rd_s and not args.filter else None},
             },
+            "configs_extra": extra,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "pcie_fanout": fan,

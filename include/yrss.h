@@ -151,7 +151,11 @@ void yrss_fini(yrss_ctx *ctx);
  * Dispatches of one context share its compaction workspace: a dispatch on a
  * different stream than the context's previous one waits (on the device) for
  * the work already queued there, so streams may be mixed freely; dispatches
- * on one stream pay nothing for this.  yrss_fini drains the device. */
+ * on one stream pay nothing for this.  yrss_fini drains the device.
+ * Stream lifetime: the context remembers the stream of its last device batch
+ * (the switch above, and yrss_status / yrss_fault_info synchronise it), so
+ * that stream must stay alive until the context's next dispatch on another
+ * stream, its next yrss_status / yrss_fault_info, or yrss_fini. */
 int yrss_dispatch_dev(yrss_ctx *ctx, const uint8_t *d_win, uint32_t win_stride,
                       const uint16_t *d_len, uint32_t n, int16_t *d_q,
                       uint32_t *d_hash, uint32_t *d_qidx, uint32_t *d_qstart,
@@ -473,7 +477,9 @@ int yrss_worker_submit_windows(yrss_ctx *ctx, const uint8_t *win, uint32_t strid
                                uint64_t *ticket);
 /* 0: the burst is done and its outputs in place; -EAGAIN: not yet (wait = 0);
  * -EFAULT: a mbuf or its data lies outside every registered range;
- * -ETIMEDOUT: waited 10 s (a burst takes microseconds: the GPU is hung). */
+ * -ETIMEDOUT: waited 10 s (a burst takes microseconds: the GPU is hung).  The
+ * context is then marked hung: yrss_fini neither waits for the device nor
+ * frees memory a still-running kernel may write (it is left to process exit). */
 int yrss_worker_poll(yrss_ctx *ctx, uint64_t ticket, int wait);
 /* Stop the kernel and free the ring (also done by yrss_fini). */
 int yrss_worker_stop(yrss_ctx *ctx);
@@ -528,6 +534,10 @@ int yrss_fanout_route(uint64_t ticket, uint32_t nctx, uint32_t *ctx, uint64_t *c
                                          where = span, value = bucket                        */
 #define YRSS_FAULT_COUNT_SLOT     4   /* parse count slot beyond LDS: where = wave, value = slot */
 #define YRSS_FAULT_STAGE          5   /* scatter stage slot out of range: where = packet     */
+#define YRSS_FAULT_LINE_CAPACITY  6   /* a line-scatter kernel launched for more buckets than
+                                         its per-bucket arrays hold (the host refuses such a
+                                         plan with -EINVAL; the kernel checks again at entry
+                                         and leaves): where = buckets, value = its capacity */
 struct yrss_fault {
     uint32_t code;     /* YRSS_FAULT_*                                   */
     uint32_t kernel;   /* YRSS_K_* of the kernel whose guard fired       */

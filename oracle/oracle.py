@@ -85,6 +85,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_bench_dispatch.restype = ctypes.c_uint64
         L.oracle_bench_dispatch.argtypes = [vp, u32, vp, u32, ctypes.POINTER(OracleCfg), u32,
                                             ctypes.c_int]
+        L.oracle_bench_window.restype = ctypes.c_uint64
+        L.oracle_bench_window.argtypes = [vp, u32, vp, u32, ctypes.POINTER(OracleCfg),
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                          ctypes.c_uint64, vp]
         _lib = L
     return _lib
 
@@ -203,6 +207,19 @@ def bench_dispatch(win, stride, lens, c: OracleCfg, reps: int, fast: bool = Fals
     lens = np.ascontiguousarray(lens).view(np.uint16)
     return lib().oracle_bench_dispatch(win.ctypes.data, stride, lens.ctypes.data, int(lens.size),
                                        ctypes.byref(c), reps, 1 if fast else 0)
+
+
+def bench_window(win, stride, lens, c: OracleCfg, fast: bool, fnptr: bool, start_ns: int,
+                 end_ns: int):
+    """Dispatch passes over the sample from CLOCK_MONOTONIC start_ns until
+    end_ns (time.monotonic_ns()), inlined or through the registered-dispatcher
+    function pointer (ff_dpdk_if.c:1078-1079).  (packets, first ns, last ns)."""
+    lens = np.ascontiguousarray(lens).view(np.uint16)
+    out = np.zeros(3, np.uint64)
+    lib().oracle_bench_window(win.ctypes.data, stride, lens.ctypes.data, int(lens.size),
+                              ctypes.byref(c), 1 if fast else 0, 1 if fnptr else 0,
+                              start_ns, end_ns, out.ctypes.data)
+    return int(out[0]), int(out[1]), int(out[2])
 
 
 def kni_bitmap(ports: str | None) -> np.ndarray:

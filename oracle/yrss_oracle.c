@@ -29,6 +29,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../include/yrss_synth.h"
 
@@ -277,6 +278,98 @@ uint64_t oracle_bench_dispatch(const uint8_t *win, uint32_t stride, const uint16
                                        &hashed);
             sum += (uint64_t)q * 0x9E3779B97F4A7C15ull + h;
         }
+    return sum;
+}
+
+/* The reference calls its dispatcher through a function pointer registered
+ * with ff_regist_packet_dispatcher: `int ret = (*packet_dispatcher)(data, len,
+ * queue_id, nb_queues)` (ff_dpdk_if.c:1078-1079, dispatch_func_t at
+ * ff_api.h:167-168), and toeplitz_dispatch reads its knobs from the global
+ * ff_global_cfg.  These wrappers have that signature and read a file-scope
+ * config; g_dispatcher is volatile so the compiler cannot inline the call. */
+static const struct oracle_cfg *g_cfg;
+static uint32_t g_tbl[12][256];
+
+static int dispatcher_bit_serial(void *data, uint16_t len, uint16_t queue_id, uint16_t nb_queues)
+{
+    uint32_t h;
+    int hashed;
+    (void)queue_id;
+    (void)nb_queues;
+    return dispatch_one((const uint8_t *)data, len, g_cfg, NULL, &h, &hashed);
+}
+
+static int dispatcher_table(void *data, uint16_t len, uint16_t queue_id, uint16_t nb_queues)
+{
+    uint32_t h;
+    int hashed;
+    (void)queue_id;
+    (void)nb_queues;
+    return dispatch_one((const uint8_t *)data, len, g_cfg, (const uint32_t(*)[256])g_tbl, &h,
+                        &hashed);
+}
+
+typedef int (*oracle_dispatch_fn)(void *data, uint16_t len, uint16_t queue_id, uint16_t nb_queues);
+static oracle_dispatch_fn volatile g_dispatcher;
+
+static uint64_t mono_ns(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+/* CPU-baseline window with a wall-clock deadline, so that every process of a
+ * multi-core cell runs over the same stretch of time: spin until start_ns
+ * (CLOCK_MONOTONIC), then pass over the sample packet by packet until end_ns
+ * (checked every 4096 packets).  call = 0: dispatch_one inlined, as
+ * oracle_bench_dispatch; call = 1: through the registered-dispatcher function
+ * pointer, as process_packets calls it.  out = {packets, first ns, last ns}.
+ * Returns a checksum so the work cannot be elided. */
+uint64_t oracle_bench_window(const uint8_t *win, uint32_t stride, const uint16_t *len,
+                             uint32_t n, const struct oracle_cfg *c, int fast, int call,
+                             uint64_t start_ns, uint64_t end_ns, uint64_t out[3])
+{
+    static uint32_t tbl[12][256];
+    if (fast) {
+        oracle_build_tables(c->keylen, c->key, tbl);
+        memcpy(g_tbl, tbl, sizeof(tbl));
+    }
+    g_cfg = c;
+    g_dispatcher = fast ? dispatcher_table : dispatcher_bit_serial;
+    while (mono_ns() < start_ns)
+        ;
+    const uint64_t t0 = mono_ns();
+    uint64_t sum = 0, done = 0, t1 = t0;
+    uint32_t i = 0;
+    for (;;) {
+        const uint32_t e = i + 4096u < n ? i + 4096u : n;
+        done += e - i;
+        if (call) {
+            for (; i < e; ++i) {
+                const int q = g_dispatcher((void *)(win + (size_t)i * stride), len[i], 0,
+                                           (uint16_t)c->nb_queues);
+                sum += (uint64_t)q * 0x9E3779B97F4A7C15ull;
+            }
+        } else {
+            for (; i < e; ++i) {
+                uint32_t h;
+                int hashed;
+                const int q = dispatch_one(win + (size_t)i * stride, len[i], c,
+                                           fast ? (const uint32_t(*)[256])tbl : NULL, &h,
+                                           &hashed);
+                sum += (uint64_t)q * 0x9E3779B97F4A7C15ull + h;
+            }
+        }
+        if (i == n)
+            i = 0;
+        t1 = mono_ns();
+        if (t1 >= end_ns)
+            break;
+    }
+    out[0] = done;
+    out[1] = t0;
+    out[2] = t1;
     return sum;
 }
 

@@ -25,6 +25,63 @@ def test_library_exports_every_header_function():
         assert getattr(lib, n) is not None
 
 
+def test_shipping_library_has_no_test_or_measurement_paths():
+    """libyrss.so carries no test hook and no measurement build (VERDICT r04
+    item 7): the yrss_debug_* hooks of include/yrss_test_hooks.h live in
+    libyrss_test.so only, the phase clock (YRSS_PROF_LINES) only in
+    tools/build_ab_lib.sh builds, and no hook reads the environment."""
+    hooks = abi.header_functions(abi.REPO_DIR / "include" / "yrss_test_hooks.h")
+    assert hooks == ["yrss_debug_line_groups", "yrss_debug_worker_inject"]
+    ship = subprocess.run(["nm", "-D", "--defined-only", str(abi.LIB_PATH)],
+                          capture_output=True, text=True, check=True).stdout
+    assert not re.findall(r"\bT (yrss_debug_\w+)", ship)
+    data = abi.LIB_PATH.read_bytes()
+    for s in (b"YRSS_WORKER_INJECT", b"g_line_prof", b"yrss_debug_"):
+        assert s not in data, s
+    test = subprocess.run(["nm", "-D", "--defined-only", str(abi.TEST_LIB_PATH)],
+                          capture_output=True, text=True, check=True).stdout
+    assert sorted(re.findall(r"\bT (yrss_debug_\w+)", test)) == hooks
+    # the measurement macro refuses a product build
+    src = (abi.REPO_DIR / "yastack_amd" / "csrc" / "yrss.hip").read_text()
+    assert "#if defined(YRSS_PROF_LINES) && !defined(YRSS_TOOLS_BUILD)\n#error" in src
+    assert "YRSS_NO_CNT_FLUSH" not in src and "getenv(\"YRSS_WORKER_INJECT\")" not in src
+
+
+def test_close_of_a_timed_out_context_does_not_wait():
+    """A context whose call returned -ETIMEDOUT (a hung GPU) is closed
+    without yrss_fault_info, which would synchronise the hung streams; the
+    C side (yrss_fini, c->hung) then skips its own drain."""
+    from yastack_amd.dispatch import SoftRss
+
+    calls = []
+
+    class FakeLib:
+        def yrss_fault_info(self, ctx, out):
+            calls.append("fault_info")
+            return 0
+
+        def yrss_fini(self, ctx):
+            calls.append("fini")
+
+    eng = SoftRss.__new__(SoftRss)
+    eng._lib = FakeLib()
+    eng._ctx = ctypes.c_void_p(0x1000)
+    with pytest.raises(abi.YrssError):
+        eng._ck(-errno.ETIMEDOUT, "yrss_worker_poll")
+    eng.close()
+    assert calls == ["fini"]
+    eng2 = SoftRss.__new__(SoftRss)
+    eng2._lib = FakeLib()
+    eng2._ctx = ctypes.c_void_p(0x1000)
+    calls.clear()
+    eng2.close()
+    assert calls == ["fault_info", "fini"]
+    src = (abi.REPO_DIR / "yastack_amd" / "csrc" / "yrss.hip").read_text()
+    fini = src[src.index("void yrss_fini(yrss_ctx *c)"):]
+    fini = fini[:fini.index("\n}\n")]
+    assert fini.index("if (c->hung)") < fini.index("hipDeviceSynchronize")
+
+
 def test_library_is_gfx950_code_object():
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", str(abi.LIB_PATH)],
                          capture_output=True, text=True).stdout

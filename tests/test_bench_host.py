@@ -48,7 +48,43 @@ def test_cbench_rows_median_and_spread():
 
 def test_gpu_placement_unknown_device():
     p = bench.gpu_placement("ffff:ff:ff")
-    assert p == {"gpu_node": None, "dispatch_cpu": None}
+    assert p["gpu_node"] is None and p["dispatch_cpu"] is None
+
+
+def test_gpu_placement_takes_a_physical_core_off_the_first(monkeypatch, tmp_path):
+    """The dispatcher goes on a physical core of the GPU's node (the first SMT
+    sibling of its core), never the node's first core nor that core's twin
+    (CPU 128 / 192 were the twins of CPUs 0 / 64)."""
+    sysfs = {"/sys/bus/pci/devices/0000:0d:00.0/numa_node": "0\n",
+             "/sys/devices/system/node/node0/cpulist": "0-7,16-23\n"}
+    for c in range(8):   # cores 0..7, twins 16..23
+        for cpu in (c, c + 16):
+            sysfs[f"/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list"] = \
+                f"{c},{c + 16}\n"
+    real = bench.Path
+
+    class FakePath(type(real())):
+        def read_text(self):
+            key = str(self)
+            if key in sysfs:
+                return sysfs[key]
+            raise OSError(key)
+
+    monkeypatch.setattr(bench, "Path", FakePath)
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda pid: set(range(32)))
+    p = bench.gpu_placement("0000:0d:00")
+    assert p["gpu_node"] == 0
+    assert p["dispatch_cpu"] in range(1, 8) and p["dispatch_cpu_is_first_sibling"]
+    assert p["dispatch_cpu_siblings"] == [p["dispatch_cpu"], p["dispatch_cpu"] + 16]
+
+
+def test_cpu_worker_windows_are_common():
+    """Every process of a multi-core cell runs over one CLOCK_MONOTONIC window
+    (VERDICT r04 weak 6): two processes, overlap near 1, and a cell below
+    OVERLAP_MIN would carry a flag."""
+    cell = bench._cpu_run("udp4", "table", 0.3, ["-", "-"], runs=2)
+    assert cell["runs"] == 2 and cell["overlap"] > 0.5
+    assert ("flag" in cell) == (cell["overlap"] < bench.OVERLAP_MIN)
 
 
 def test_cpu_baseline_cells_carry_spread():
@@ -63,6 +99,11 @@ def test_cpu_baseline_cells_carry_spread():
             for cores, cell in cells.items():
                 assert cell["min"] <= cell["mpps"] <= cell["max"], (prof, var, cores, cell)
                 assert cell["runs"] == bench.CPU_RUNS and 0.0 <= cell["overlap"] <= 1.0
+    # the reference's call form (function pointer) and the inlined one, 1 core
+    head = cpu["by_profile"][args.profile]
+    assert cpu["value"] == head["bit_serial_fnptr"]["1"]["mpps"]
+    assert cpu["value_inlined"] == head["bit_serial"]["1"]["mpps"]
+    assert isinstance(cpu["flagged_cells"], list)
     q, _ = bench.cpu_quota()
     assert cpu["all_cores"]["cores"] == max(q, cpu["per_gpu_share"]["cores"])
     assert "quota" in cpu["all_cores"]["note"]

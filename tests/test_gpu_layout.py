@@ -186,6 +186,40 @@ def test_scatter_xcd_mapping(dev, oracle_mod, cfg, xcd):
             check(eng, oracle_mod, cfg, profile, 777777, first=31)
 
 
+def test_line_scatter_capacity_is_enforced(dev, oracle_mod):
+    """The line scatter's kG = 2 instantiation holds 128 buckets' layout words
+    (line_nb_max).  Forced onto 256 buckets (round 4's hang) it is refused by
+    the host with -EINVAL before anything runs; launched past that check it
+    reports YRSS_FAULT_LINE_CAPACITY at kernel entry and leaves, with q and
+    hash still exact.  Run once, through libyrss_test.so's hook."""
+    import errno
+
+    cfg = (255, 255, 1, 0)
+    n = 1 << 20
+    with SoftRss(*cfg, device=0, max_burst=0, lib_path=str(abi.TEST_LIB_PATH)) as eng:
+        lib, ctx = eng._lib, eng._ctx
+        win, lens = eng.synth(abi.SYN_TCP4, n, 5)
+        assert lib.yrss_debug_line_groups(ctx, 3, 0) == -errno.EINVAL
+        assert lib.yrss_debug_line_groups(ctx, 2, 0) == 0
+        with pytest.raises(abi.YrssError) as ei:
+            eng.dispatch_dev(win, lens, 64, n)
+        assert ei.value.errno == errno.EINVAL
+        torch.cuda.synchronize()
+        assert eng.fault_info()[0] == abi.FAULT_NONE
+        assert lib.yrss_debug_line_groups(ctx, 2, 1) == 0   # past the host check
+        res = eng.dispatch_dev(win, lens, 64, n)
+        torch.cuda.synchronize()
+        assert eng.fault_info() == (abi.FAULT_LINE_CAPACITY, abi.K_SCATTER, 256, 128)
+        w_h = win[: n * 64].cpu().numpy()
+        q_ref, h_ref = oracle_mod.dispatch_windows(w_h, 64, to_np(lens[:n], np.uint16),
+                                                   oracle_mod.cfg(*cfg))
+        assert np.array_equal(to_np(res.q[:n], np.int16), q_ref)
+        assert np.array_equal(to_np(res.hash[:n], np.uint32), h_ref)
+        # the built-in choice again: lists exact, no fault
+        assert lib.yrss_debug_line_groups(ctx, 0, 0) == 0
+        check(eng, oracle_mod, cfg, abi.SYN_TCP4, n, first=5)
+
+
 def test_tuning_rejects_bad_values(dev):
     with SoftRss(3, device=0, max_burst=0) as eng:
         for kw in ({"chunk_tiles": 3}, {"span_tiles": 6}, {"one_launch": 3}, {"scatter_xcd": 2}):

@@ -490,20 +490,22 @@ def test_device_batch_beside_other_process_worker(dev):
         assert shared < solo + 5.0, (solo, shared)
 
 
-def test_worker_guard_fault_is_per_burst(dev, oracle_mod, monkeypatch):
+def test_worker_guard_fault_is_per_burst(dev, oracle_mod):
     """A list guard that fires in one worker burst fails that burst alone
     (-EIO), with several bursts of other workgroups in flight at once; the
     record names it and the bursts around it stay bit-exact (ADVICE r03:
-    the context-wide record used to be taken by whichever poll came first)."""
+    the context-wide record used to be taken by whichever poll came first).
+    Driven through libyrss_test.so's yrss_debug_worker_inject (the shipping
+    library has no injection path)."""
     import errno
 
-    monkeypatch.setenv("YRSS_WORKER_INJECT", "5")   # test hook: ticket 5 fires a guard
     cfg = (8, 8, 1, 0)
     nb, per = 12, 40
     frames = _frames(oracle_mod, nb * per, 77)
     pool, ptrs, _ = _fake_mbufs(frames)
     q_all, h_all, _, _ = _expect(oracle_mod, frames, cfg)
-    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+    with SoftRss(*cfg, device=0, max_burst=0, lib_path=str(abi.TEST_LIB_PATH)) as eng:
+        assert eng._lib.yrss_debug_worker_inject(eng._ctx, 5) == 0   # ticket 5 fires a guard
         eng.register_host_memory(pool.ctypes.data, pool.nbytes)
         eng.worker_start(16, 4)
         tickets = [eng.worker_submit(ptrs[i * per:(i + 1) * per]) for i in range(nb)]

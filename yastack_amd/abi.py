@@ -17,6 +17,9 @@ from pathlib import Path
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
 LIB_PATH = PKG_DIR / "_lib" / "libyrss.so"
+# the same sources built with -DYRSS_TEST_HOOKS (include/yrss_test_hooks.h):
+# loaded by the GPU tests that drive the fault guards, never by the product
+TEST_LIB_PATH = PKG_DIR / "_lib" / "libyrss_test.so"
 HEADER_PATH = REPO_DIR / "include" / "yrss.h"
 
 RSS_KEY_LEN = 40
@@ -34,7 +37,7 @@ K_BURST, K_WORKER = 8, 9            # kernel ids of fault records only
 
 # device-side fault record codes (yrss_fault_info)
 FAULT_NONE, FAULT_SCAN_TIMEOUT, FAULT_LIST_RANGE, FAULT_COUNT_MISMATCH, FAULT_COUNT_SLOT, \
-    FAULT_STAGE = range(6)
+    FAULT_STAGE, FAULT_LINE_CAPACITY = range(7)
 
 # protocol_filter classes (ff_dpdk_kni.h:34-38) + boundary outcomes
 FILTER_UNKNOWN, FILTER_ARP, FILTER_KNI, FILTER_TRUNC, FILTER_LOOP = -1, 1, 2, -2, -3
@@ -233,6 +236,12 @@ _PROTOS = {
                                         ctypes.POINTER(RouteResult)]),
 }
 
+# include/yrss_test_hooks.h (libyrss_test.so)
+_TEST_PROTOS = {
+    "yrss_debug_worker_inject": (ctypes.c_int, [_vp, ctypes.c_uint64]),
+    "yrss_debug_line_groups": (ctypes.c_int, [_vp, _u32, ctypes.c_int]),
+}
+
 _lib = None
 _libs: dict[str, ctypes.CDLL] = {}
 
@@ -270,6 +279,11 @@ def load(path: str | os.PathLike | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    for name, (res, args) in _TEST_PROTOS.items():   # libyrss_test.so only
+        if hasattr(lib, name):
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
     _libs[key] = lib
     if path is None:
         _lib = lib

@@ -44,6 +44,9 @@
 
 #include "yrss.h"
 #include "yrss_synth.h"
+#ifdef YRSS_TEST_HOOKS
+#include "yrss_test_hooks.h"
+#endif
 
 namespace {
 
@@ -684,10 +687,8 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         }
         while (j < kmax) {
             const uint32_t col = g0 + w + j * W;
-#ifndef YRSS_NO_CNT_FLUSH   // measurement builds only: the flush's cost (lists then wrong)
             if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords)
                 P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
-#endif
             b += kBlock / kWaves;
             while (b >= P.nb) {
                 b -= P.nb;
@@ -1216,6 +1217,15 @@ constexpr uint32_t line_tab_max(uint32_t g) { return kLineBlock * line_tab_regs(
 // (carried lines, layout) is large enough to amortise over twice the packets
 // (q255 scatter 93 -> 75 us; at 64 buckets kG = 4 cost 3-4 us, r03 A/B).
 constexpr uint32_t line_span_max(uint32_t g) { return kLineBlock * 8u * g; }
+// Wave 0 holds the per-bucket totals and span prefixes a bucket to a lane, in
+// line_bucket_regs(kG) registers each: the kernel serves nb <= 64 x that.
+// A launch past it would leave the other buckets' layout words unwritten, and
+// the tagging loop bounded by them would run ~2^31 iterations of dropped LDS
+// stores (round 4's hang): the host refuses such a plan
+// (-EINVAL) and the kernel checks again at entry.
+constexpr uint32_t line_bucket_regs(uint32_t g) { return g == 2u ? 2u : 8u; }
+constexpr uint32_t line_nb_max(uint32_t g) { return 64u * line_bucket_regs(g); }
+static_assert(line_nb_max(4) <= (uint32_t)kLineBlock, "tagging: a thread to a bucket at least");
 
 
 struct LineParams {
@@ -1297,6 +1307,9 @@ __device__ __forceinline__ void load_groups(const uint16_t *a, uint32_t p0, uint
     }
 }
 
+#if defined(YRSS_PROF_LINES) && !defined(YRSS_TOOLS_BUILD)
+#error "YRSS_PROF_LINES is a measurement build: tools/build_ab_lib.sh only, never libyrss.so"
+#endif
 #ifdef YRSS_PROF_LINES
 // measurement builds only (tools/line_prof.py): per workgroup and span, the
 // realtime clock at each phase boundary, read by thread 0
@@ -1319,6 +1332,14 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
     const uint32_t nb = P.nb, t = threadIdx.x, lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    // Capacity, checked before any barrier (the condition is uniform): a
+    // plan past what this instantiation holds reports and leaves, instead of
+    // running on unwritten per-bucket words (see line_nb_max)
+    if (nb > line_nb_max(kG) || (nb << P.gshift) > line_tab_max(kG)) {
+        if (t == 0)
+            report_fault(P.fault, YRSS_FAULT_LINE_CAPACITY, YRSS_K_SCATTER, nb, line_nb_max(kG));
+        return;
+    }
     const LineLds o = line_lds(nb, P.gshift, P.lmax);
 #ifdef YRSS_PROF_LINES
     if (t == 0 && blockIdx.x < 2048u)   // kernel entry, slot 7 of span 0
@@ -1367,7 +1388,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // wave 0 also holds, a bucket to a lane, each bucket's prefix at the
     // span's first chunk and at its end, so it lays the span out from
     // registers while the other waves write the prefix table
-    constexpr uint32_t kBI = kG == 2u ? 2u : 8u;   // nb <= 64 kBI
+    constexpr uint32_t kBI = line_bucket_regs(kG);   // nb <= 64 kBI (checked at entry)
     constexpr uint32_t kLineTabRegs = line_tab_regs(kG);
     uint32_t pt[kLineTabRegs], w0s[kBI], w0e[kBI];
     auto load_span = [&](uint32_t g, u32x4 (&pk)[kG], u32x4 (&qk)[kG]) {
@@ -1426,7 +1447,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // Every bucket block's total is loaded before the first is scanned: one
     // round trip, not one per 64 buckets.
     if (wave == 0) {
-        constexpr uint32_t kTB = kG == 2u ? 2u : 8u;   // nb <= 64 kTB
+        constexpr uint32_t kTB = line_bucket_regs(kG);   // nb <= 64 kTB (checked at entry)
         uint32_t tv[kTB];
 #pragma unroll
         for (uint32_t i = 0; i < kTB; ++i) {
@@ -1586,7 +1607,8 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             load_span(g + 1u, pkn, qkn);
         if (tj < tk) {
             const uint32_t b = opaque(tb);   // (addresses not hoisted: registers)
-            const uint32_t l0 = lsl[b], l1 = L ? lsl[b + 1u] : 0u, v0 = cs[b], e1 = ve[b];
+            // (bounded by the span's line count whatever the words say)
+            const uint32_t l0 = lsl[b], l1 = L ? min(lsl[b + 1u], L) : 0u, v0 = cs[b], e1 = ve[b];
             for (uint32_t l = l0 + tj; l < l1; l += tk) {
                 const uint32_t gl = l - l0 + (v0 >> 4);
                 const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
@@ -2334,7 +2356,7 @@ struct WorkerParams {
     uint32_t *fault;     // [nblocks] device: gather fault of the current burst
     uint32_t *brec;      // [nblocks][4] device: guard record of the current burst
     uint32_t *srec;      // [nslots][4] host-coherent: guard record of the slot's burst
-    uint64_t inject;     // tests only (YRSS_WORKER_INJECT): ticket whose burst fires a guard
+    uint64_t inject;     // -DYRSS_TEST_HOOKS builds only: ticket whose burst fires a guard
     uint64_t *ptrs;      // [nslots][kWorkerMaxBurst] pinned: mbuf or frame data pointers
     uint16_t *lens;      // [nslots][kWorkerMaxBurst] pinned: frame data_len (frames mode)
     uint8_t *win;        // device scratch [nblocks][kWorkerMaxBurst * 80]
@@ -2467,8 +2489,10 @@ __global__ __launch_bounds__(kSmallBlock) void yrss_burst_worker(WorkerParams W)
         ParseParams P = W.P;
         P.n = n;
         P.fault = W.brec + 4u * blockIdx.x;   // this burst's own record
+#ifdef YRSS_TEST_HOOKS   // libyrss_test.so only: the per-burst fault path's test
         if (t == W.inject && threadIdx.x == 0)
             report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_WORKER, (uint32_t)t, 0xdeadu);
+#endif
         P.win = W.win + (size_t)blockIdx.x * kWorkerMaxBurst * YRSS_WIN_FULL;
         P.len = W.len + (size_t)blockIdx.x * kWorkerMaxBurst;
         P.stride = YRSS_WIN_FULL;
@@ -2696,7 +2720,6 @@ struct yrss_ctx {
         uint32_t *fault = nullptr;                         // device [nblocks]
         uint32_t *brec = nullptr;                          // device [nblocks][4]
         uint32_t *srec = nullptr, *d_srec = nullptr;       // host-coherent [nslots][4]
-        uint64_t inject = 0;                               // tests only
         uint64_t *ptrs = nullptr, *d_ptrs = nullptr;       // pinned
         uint16_t *lens = nullptr, *d_lens = nullptr;       // pinned (frames mode)
         int16_t *q = nullptr, *d_q = nullptr;
@@ -2734,6 +2757,17 @@ struct yrss_ctx {
     double ms[YRSS_K_COUNT] = {0, 0, 0};
     uint32_t launches[YRSS_K_COUNT] = {0, 0, 0};
     std::vector<float> durs[YRSS_K_COUNT];   // per-launch ms since yrss_timing_enable
+    // A call on this context saw the GPU not finish its work (-ETIMEDOUT):
+    // yrss_fini then neither waits for the device nor frees memory a running
+    // kernel may still touch (the allocations are left to process exit).
+    bool hung = false;
+    // Test hooks (set only through the yrss_debug_* entry points of a
+    // -DYRSS_TEST_HOOKS build, libyrss_test.so; always 0 in libyrss.so).
+    struct Debug {
+        uint64_t worker_inject = 0;   // ticket whose worker burst fires a list guard
+        uint32_t line_groups = 0;     // force the line scatter's kG (2 or 4)
+        uint32_t skip_line_check = 0; // launch a line scatter the host check refuses
+    } dbg;
 };
 
 namespace {
@@ -2850,6 +2884,7 @@ ScatterLds scatter_lds(uint32_t nb)
 // than a span can be (batches past ~2^29 packets) or the LDS would not fit.
 struct LinePlan {
     bool ok, packed;
+    bool fits;   // nb within the kernel's per-bucket capacity (line_nb_max)
     uint32_t groups, gshift, seg, lmax, lds;
 };
 
@@ -2857,7 +2892,10 @@ LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
 {
     LinePlan p{};
     const uint32_t nb = c->nb, cshift = lay.ct_shift + 6u;
-    p.groups = nb > 128u ? 4u : 2u;
+    p.groups = nb > line_nb_max(2) ? 4u : 2u;
+    if (c->dbg.line_groups)   // test builds only (yrss_debug_line_groups)
+        p.groups = c->dbg.line_groups;
+    p.fits = nb <= line_nb_max(p.groups) && nb <= (uint32_t)kLineBlock;
     const uint32_t smax = line_span_max(p.groups);
     if (lay.chunk > smax || nb > (uint32_t)kLineBlock)
         return p;
@@ -3120,6 +3158,7 @@ const char *fault_name(uint32_t code)
     case YRSS_FAULT_COUNT_MISMATCH: return "span histogram differs from the parse counts";
     case YRSS_FAULT_COUNT_SLOT: return "parse count slot outside the wave's LDS";
     case YRSS_FAULT_STAGE: return "stage slot outside the piece";
+    case YRSS_FAULT_LINE_CAPACITY: return "line scatter launched for more buckets than it holds";
     default: return "unknown";
     }
 }
@@ -3516,6 +3555,20 @@ void yrss_fini(yrss_ctx *c)
         if (g_dispatch_ctx == c)
             g_dispatch_ctx = nullptr;
     }
+    if (c->hung) {
+        // A call already timed out on this device: draining it
+        // would block here as well.  Ask a resident worker to leave, keep
+        // every device and pinned allocation (a kernel still running may
+        // write them), and free only what the host alone uses.
+        if (c->w.on && c->w.ctl)
+            __atomic_store_n(&c->w.ctl->stop, 1u, __ATOMIC_RELEASE);
+        fprintf(stderr, "yrss: context closed after a GPU timeout: not drained, device memory "
+                        "left to process exit\n");
+        delete[] c->w.out;
+        delete[] c->w.last_out;
+        delete c;   // (shim_win stays: it may be registered for the GPU to read)
+        return;
+    }
     if (c->w.on) {
         (void)worker_halt(c);
         worker_free(c);
@@ -3652,6 +3705,10 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     // the line scatter reads q (when the bucket is not packed with the rank)
     // as 16-byte vectors
     const bool ranked = compact && lp.ok && (lp.packed || ((uintptr_t)b->q & 15u) == 0);
+    // a line scatter whose per-bucket arrays cannot hold nb is refused before
+    // anything is launched (the kernel's own entry check is the backstop)
+    if (ranked && !lp.fits && !c->dbg.skip_line_check)
+        return -EINVAL;
     if (ranked && W.rank_cap < n) {
         // the ranks' workspace grows to the largest batch seen; the old one
         // may still be read by a scatter queued on this stream
@@ -4442,7 +4499,7 @@ int worker_launch(yrss_ctx *c)
     W.fault = w.fault;
     W.brec = w.brec;
     W.srec = w.d_srec;
-    W.inject = w.inject;
+    W.inject = c->dbg.worker_inject;
     W.ptrs = w.d_ptrs;
     W.lens = w.d_lens;
     W.win = w.win;
@@ -4542,12 +4599,6 @@ int yrss_worker_start(yrss_ctx *c, uint32_t nslots, uint32_t nblocks)
     memset((void *)w.slots, 0, S * sizeof(WorkerSlot));
     memset((void *)w.done, 0, S * sizeof(uint64_t));
     memset((void *)w.srec, 0, S * 4u * sizeof(uint32_t));
-    {
-        // tests only: the burst of this ticket fires a list guard (the
-        // per-burst fault path, tests/test_gpu_worker.py)
-        const char *inj = getenv("YRSS_WORKER_INJECT");
-        w.inject = inj ? strtoull(inj, nullptr, 10) : 0u;
-    }
     for (uint32_t b = 0; b < nblocks; ++b)
         w.next[b] = b + 1u;            // tickets start at 1; block b serves b+1, b+1+B, ...
     memset((void *)w.ctl, 0, sizeof(WorkerCtl));
@@ -4694,8 +4745,10 @@ int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
             const uint64_t now = mono_ns();
             if (!t0)
                 t0 = now;
-            else if (now - t0 > 10ull * 1000000000ull)
+            else if (now - t0 > 10ull * 1000000000ull) {
+                c->hung = true;   // yrss_fini will not wait for this device
                 return -ETIMEDOUT;
+            }
         }
         __builtin_ia32_pause();
     }
@@ -4713,12 +4766,19 @@ int yrss_worker_poll(yrss_ctx *c, uint64_t ticket, int wait)
                         "per-queue lists invalid\n",
                 g[0], fault_name(g[0]), yrss_kernel_name((int)g[1]), g[2], g[3],
                 (unsigned long long)ticket);
+        // Claimed the way report_fault claims it on the device (a device batch
+        // on another stream may be storing its own record right now): the
+        // code word goes 0 -> code by compare-and-swap, and only the winner
+        // writes the fields, so a record never mixes two faults.  (A reader
+        // between the claim and the field stores sees the code with the
+        // previous, cleared fields; take_fault reads after its own sync.)
         uint32_t *r = c->d_fault_rec;
-        if (__atomic_load_n(r, __ATOMIC_ACQUIRE) == 0u) {
-            r[1] = g[1];
-            r[2] = g[2];
-            r[3] = g[3];
-            __atomic_store_n(r, g[0], __ATOMIC_RELEASE);
+        uint32_t expected = 0u;
+        if (__atomic_compare_exchange_n(r, &expected, g[0], false, __ATOMIC_ACQ_REL,
+                                        __ATOMIC_ACQUIRE)) {
+            __atomic_store_n(r + 1, g[1], __ATOMIC_RELAXED);
+            __atomic_store_n(r + 2, g[2], __ATOMIC_RELAXED);
+            __atomic_store_n(r + 3, g[3], __ATOMIC_RELEASE);
         }
         return -EIO;
     }
@@ -4795,6 +4855,29 @@ int yrss_set_tuning(yrss_ctx *c, const struct yrss_tuning *t)
     c->tune = *t;
     return 0;
 }
+
+#ifdef YRSS_TEST_HOOKS
+// Test hooks (include/yrss_test_hooks.h), compiled into libyrss_test.so only:
+// libyrss.so has neither these symbols nor the paths they drive
+// (tests/test_abi.py checks both libraries).
+int yrss_debug_worker_inject(yrss_ctx *c, uint64_t ticket)
+{
+    if (!c)
+        return -EINVAL;
+    c->dbg.worker_inject = ticket;   // read at the next worker launch
+    return 0;
+}
+
+int yrss_debug_line_groups(yrss_ctx *c, uint32_t groups, int skip_host_check)
+{
+    if (!c || (groups != 0u && groups != 2u && groups != 4u) || skip_host_check < 0 ||
+        skip_host_check > 1)
+        return -EINVAL;
+    c->dbg.line_groups = groups;
+    c->dbg.skip_line_check = (uint32_t)skip_host_check;
+    return 0;
+}
+#endif
 
 int yrss_timing_enable(yrss_ctx *c, int enable)
 {
