@@ -22,8 +22,9 @@ extern "C" {
  * per-burst fault path of yrss_worker_poll.  0 disables. */
 int yrss_debug_worker_inject(yrss_ctx *ctx, uint64_t ticket);
 
-/* Force the line scatter's instantiation (groups 2 or 4 packets-groups a
- * thread; 0 = the built-in choice).  A pairing whose per-bucket arrays cannot
+/* Force the line scatter's kernel: 1 yrss_scatter_wide, 2 or 4
+ * yrss_scatter_lines<kG> (8-packet groups a thread), 0 = the built-in choice
+ * (wide past 128 buckets, else kG = 2).  A pairing whose per-bucket arrays cannot
  * hold nb_queues + 1 buckets makes yrss_dispatch_dev return -EINVAL before
  * anything is launched; with skip_host_check = 1 it is launched anyway, and
  * the kernel's entry check must report YRSS_FAULT_LINE_CAPACITY and leave. */

@@ -337,6 +337,12 @@ uint64_t oracle_bench_window(const uint8_t *win, uint32_t stride, const uint16_t
     }
     g_cfg = c;
     g_dispatcher = fast ? dispatcher_table : dispatcher_bit_serial;
+    /* sleep, not spin, until the common start: spinning processes use up a
+     * cgroup CPU quota before the window opens, and the throttled ones then
+     * start late (round 5's first 16-core cells overlapped 0.69) */
+    const struct timespec ts = {(time_t)(start_ns / 1000000000ull), (long)(start_ns % 1000000000ull)};
+    while (clock_nanosleep(CLOCK_MONOTONIC, TIMER_ABSTIME, &ts, NULL) != 0)
+        ;
     while (mono_ns() < start_ns)
         ;
     const uint64_t t0 = mono_ns();

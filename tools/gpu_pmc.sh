@@ -16,7 +16,7 @@ P4="SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY
 out=gpurun_out/pmc_$tag.log
 : > "$out"
 for np in $qs; do
-    B="--profile tcp4 --nb-procs $np --steps 5 --warmup 2 --cpu-seconds 0 --pcie 0 --check 0 $extra"
+    B="--profile tcp4 --nb-procs $np --steps 5 --warmup 2 --cpu-seconds 0 --pcie 0 --check 0 --extra-configs= $extra"
     i=0
     for pass in "$P1" "$P2" "$P3" "$P4"; do
         i=$((i + 1))

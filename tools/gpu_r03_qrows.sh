@@ -10,7 +10,7 @@ export TMPDIR=/tmp PYTHONUNBUFFERED=1
 out=gpurun_out/qrows_$tag.log
 : > "$out"
 for np in 3 8 64 255; do
-    B="--profile tcp4 --nb-procs $np --steps 30 --warmup 10 --cpu-seconds 0 --pcie 0 --check 1048576"
+    B="--profile tcp4 --nb-procs $np --steps 30 --warmup 10 --cpu-seconds 0 --pcie 0 --check 1048576 --extra-configs="
     echo "== q$np bench" | tee -a "$out"
     timeout -k 10 240 python bench.py $B >> "$out" 2>&1 || { echo "bench q$np rc=$?"; exit 1; }
     echo "== q$np rocprof" | tee -a "$out"

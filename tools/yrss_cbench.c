@@ -107,6 +107,8 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
         fill_frames(mbufs, pool, fdata, flen);   /* outside the timed region */
     const char *so = getenv("YRSS_CBENCH_WORKER_SLOTOUT");
     const int slotout = so && atoi(so) != 0;
+    const char *wn = getenv("YRSS_CBENCH_WIN_NT");
+    const int win_nt = wn && atoi(wn) != 0;
     const char *de = getenv("YRSS_CBENCH_WORKER_DEPTH");
     const char *be = getenv("YRSS_CBENCH_WORKER_BLOCKS");
     unsigned blocks = be ? (unsigned)atoi(be) : 4u;
@@ -161,7 +163,10 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
                  * rte_eth_rx_burst in F-Stack) is part of the timed work */
                 uint8_t *w = wst + (size_t)k * B * YRSS_WIN_FULL;
                 /* software prefetch 16 windows ahead, into the next burst too
-                 * (the cbench pool is cache-cold, unlike headers just received) */
+                 * (the cbench pool is cache-cold, unlike headers just received).
+                 * YRSS_CBENCH_WIN_NT=1: the staging is written with non-temporal
+                 * 16-byte stores, so the dispatcher takes no read-for-ownership
+                 * miss on staging lines the GPU read since their last use */
                 for (uint32_t j = 0; j < B; ++j) {
                     const uint32_t a = off + j + 16u;
                     if (a < pool) {
@@ -169,8 +174,19 @@ static int run_worker(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
                         __builtin_prefetch(fdata[a] + 64);
                     }
                     const uint32_t L = flen[off + j] < YRSS_WIN_FULL ? flen[off + j] : YRSS_WIN_FULL;
-                    memcpy(w + (size_t)j * YRSS_WIN_FULL, fdata[off + j], L);
+                    if (win_nt) {
+                        /* whole 16-byte pieces: the window's bytes past L are
+                         * never read by the GPU (data_len bounds them) */
+                        const __m128i *src = (const __m128i *)fdata[off + j];
+                        __m128i *dst = (__m128i *)(w + (size_t)j * YRSS_WIN_FULL);
+                        for (uint32_t p = 0; p < (L + 15u) / 16u; ++p)
+                            _mm_stream_si128(dst + p, _mm_loadu_si128(src + p));
+                    } else {
+                        memcpy(w + (size_t)j * YRSS_WIN_FULL, fdata[off + j], L);
+                    }
                 }
+                if (win_nt)
+                    _mm_sfence();   /* the stores reach memory before the slot is published */
                 rc = yrss_worker_submit_windows(ctx, w, YRSS_WIN_FULL, flen + off, B, q_all + oo,
                                                 h_all + oo, qi_all + oo, qs[k], &tk[k]);
             } else {

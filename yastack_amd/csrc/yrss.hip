@@ -1814,6 +1814,437 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
 }
 
 // ---------------------------------------------------------------------------
+// Kernel 3 (ranked, many buckets): the lists in whole lines at two workgroups
+// per CU (round 5).  Past 128 buckets the line scatter above needs 16 384-
+// packet spans to amortise its per-bucket work, and its stage of 32-bit words
+// laid out line for line (two lines of padding a bucket) then holds 145 KB of
+// LDS: one workgroup per CU, whose copy-out (the chip's list writes) and
+// placement (LDS) cannot overlap another's.  The list writes alone take
+// 13-15 us for 2^24 packets at any bucket count (tools/list_write_bw.hip,
+// profiles/r05_list_write_bw.log), against 52 us for the kernel at 256: the
+// phases, not the store pattern, are the cost.  This kernel fits 8192-packet
+// spans of up to 320 buckets in <= 80 KB:
+// - the stage is compact and 16-bit: the span's packets sorted by bucket as
+//   offsets from the span's first packet (8192 x 2 bytes), no line padding;
+//   bucket b's packets start at stage index sb[b] (an exclusive scan of the
+//   span's counts), a packet's index is tab[b][chunk] + rank as before;
+// - the words carried from earlier spans (a bucket's unfinished last line,
+//   <= 15 words) stay 32-bit in a carry array of two sets, one read by this
+//   span's copy-out and one written for the next, so the carry needs no
+//   barrier of its own;
+// - a list word at adjusted position a of bucket b is the carried word
+//   cb[b][a - cs[b]] below ce[b], else p0 + stage[sb[b] + a - ce[b]];
+// - wave 0 lays the next span out right after its own placement, before the
+//   copy-out barrier, so a span takes two barriers.
+// Same outputs, checks and fault records as yrss_scatter_lines; always reads
+// the rank beside q (no 16-bit packing past 64 buckets at these chunks).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kWideG = 2;                             // 8-packet groups a thread
+constexpr uint32_t kWideSpan = kLineBlock * 8u * kWideG;   // 8192 packets
+constexpr uint32_t kWideBI = 5;                            // buckets a wave-0 lane holds
+constexpr uint32_t kWideNbMax = 64u * kWideBI;             // 320 (nb <= 257 in use)
+constexpr uint32_t kWideTabRegs = 5;                       // nb x span chunks <= 2560
+constexpr uint32_t kWideTabMax = kLineBlock * kWideTabRegs;
+
+struct WideLds {
+    uint32_t start, cs, ve, ce, sb, rb, lsl, misc, tab, cb, ltag, stg, words;
+};
+__host__ __device__ inline WideLds wide_lds(uint32_t nb, uint32_t gshift, uint32_t lmax,
+                                            uint32_t seg)
+{
+    WideLds L;
+    uint32_t o = 0;
+    auto take = [&](uint32_t w) {
+        const uint32_t at = o;
+        o = (o + w + 3u) & ~3u;
+        return at;
+    };
+    L.start = take(nb);
+    L.cs = take(2u * nb);    // first valid adjusted position (carried words first)
+    L.ve = take(2u * nb);    // end adjusted position
+    L.ce = take(2u * nb);    // first position of the span's own packets
+    L.sb = take(2u * nb);    // stage index of the bucket's first packet
+    L.rb = take(2u * nb);    // prefix table row bias (to stage indices)
+    L.lsl = take(2u * (nb + 1u));   // first list line of each bucket in the span
+    L.misc = take(8);
+    L.tab = take(nb * ((1u << gshift) + 1u));
+    L.cb = take(2u * 16u * nb);     // carried words, two sets
+    L.ltag = take(lmax);            // bucket | copy mode << 30 per line
+    L.stg = take((seg + 2u) / 2u);  // seg 16-bit offsets + the spare
+    L.words = o;
+    return L;
+}
+
+// (second bound: waves per SIMD, 4 = two 512-thread workgroups a CU, <= 128 VGPRs)
+__global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
+    const uint32_t nb = P.nb, t = threadIdx.x, lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    // capacity, before any barrier (uniform): see line_nb_max
+    if (nb > kWideNbMax || (nb << P.gshift) > kWideTabMax || P.seg > kWideSpan) {
+        if (t == 0)
+            report_fault(P.fault, YRSS_FAULT_LINE_CAPACITY, YRSS_K_SCATTER, nb, kWideNbMax);
+        return;
+    }
+    const WideLds o = wide_lds(nb, P.gshift, P.lmax, P.seg);
+#ifdef YRSS_PROF_LINES
+    if (t == 0 && blockIdx.x < 2048u)
+        g_line_prof[(blockIdx.x * 8u) * 8u + 7u] = __builtin_amdgcn_s_memrealtime();
+#endif
+    uint32_t *start = lsm + o.start, *misc = lsm + o.misc, *tab = lsm + o.tab;
+    uint32_t *const cs_sets = lsm + o.cs, *const ve_sets = lsm + o.ve, *const ce_sets = lsm + o.ce;
+    uint32_t *const sb_sets = lsm + o.sb, *const rb_sets = lsm + o.rb, *const lsl_sets = lsm + o.lsl;
+    uint32_t *const cb_sets = lsm + o.cb, *ltag = lsm + o.ltag;
+    uint16_t *stg = reinterpret_cast<uint16_t *>(lsm + o.stg);
+    const uint32_t cap = P.seg;   // the spare stage slot
+    const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 15u);
+    const uint32_t nsp = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
+    const uint32_t r = xcd_block(P.xcd), G = gridDim.x;
+    const uint32_t g0 = (uint32_t)((uint64_t)r * nsp / G);
+    const uint32_t g1 = (uint32_t)((uint64_t)(r + 1u) * nsp / G);
+    const uint32_t ncs = 1u << P.gshift, ntab = nb << P.gshift, rs = ncs + 1u;
+    auto prefix = [&](uint32_t b, uint32_t c) {
+        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : P.totals[b];
+    };
+    auto span_end = [&](uint32_t g) {
+        const uint64_t e = (uint64_t)g * P.seg + P.seg;
+        return e < P.n ? (uint32_t)e : P.n;
+    };
+    uint32_t pre0 = 0;
+    const ListOut lout = list_out(P.qidx, P.n);
+    // the current span's streams and the next span's (issued in (b), waited
+    // for before the copy-out, then moved into the current set: no wait)
+    u32x4 pk[kWideG], qk[kWideG], pkn[kWideG], qkn[kWideG];
+    // wave 0, a bucket to a lane: the prefix at the end of the span it lays
+    // out next (its start is the previous span's end, already in ve)
+    uint32_t pt[kWideTabRegs], w0e[kWideBI];
+    auto load_span = [&](uint32_t g, u32x4 (&lk)[kWideG], u32x4 (&lq)[kWideG]) {
+        const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
+        load_groups(P.rank, p0, pe, tt, lk);
+        load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, lq);
+        const uint32_t c0 = g << P.gshift;
+        if (wave == 0) {
+            const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
+            const __amdgpu_buffer_rsrc_t rtot = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint32_t *>(P.totals), 0, (int)(nb * 4u), kRsrcWord3);
+            const bool inner = c0 + ncs < P.nchunk;
+            const uint32_t ll = opaque(lane);
+#pragma unroll
+            for (uint32_t i = 0; i < kWideBI; ++i) {
+                if (i * kWave < nb) {   // (uniform)
+                    const uint32_t b = i * kWave + ll;
+                    w0e[i] = inner ? __builtin_amdgcn_raw_buffer_load_b32(
+                                         rs0, (int)(b * P.ncol * 4u), (int)((c0 + ncs) * 4u), 0)
+                                   : __builtin_amdgcn_raw_buffer_load_b32(rtot, (int)(b * 4u), 0, 0);
+                }
+            }
+        }
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
+        const uint32_t vo = ((tt >> P.gshift) * P.ncol + (tt & (ncs - 1u))) * 4u;
+        const uint32_t step = (kLineBlock >> P.gshift) * P.ncol * 4u;
+#pragma unroll
+        for (uint32_t k = 0; k < kWideTabRegs; ++k)
+            if (k * kLineBlock < ntab)   // (uniform)
+                pt[k] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)vo, (int)(c0 * 4u + k * step), 0);
+    };
+    if (P.early && g0 < g1) {
+        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
+        load_span(g0, pk, qk);
+    }
+    // list starts (exclusive scan of totals), every block's total loaded at once
+    if (wave == 0) {
+        uint32_t tv[kWideBI];
+#pragma unroll
+        for (uint32_t i = 0; i < kWideBI; ++i) {
+            const uint32_t b = i * kWave + lane;
+            tv[i] = i * kWave < nb && b < nb ? P.totals[b] : 0u;
+        }
+        uint32_t carry = 0, nzb = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kWideBI; ++i) {
+            if (i * kWave >= nb)   // (uniform)
+                break;
+            const uint32_t b = i * kWave + lane;
+            const uint32_t x0 = tv[i];
+            nzb += (uint32_t)__popcll(__ballot(x0 != 0u));
+            const uint32_t x = wave_incl_scan(x0, lane);
+            if (b < nb) {
+                start[b] = carry + x - x0;
+                if (blockIdx.x == 0)
+                    P.qstart[b] = carry + x - x0;
+            }
+            carry += __shfl(x, kWave - 1, kWave);
+        }
+        if (lane == 0) {
+            if (blockIdx.x == 0)
+                P.qstart[nb] = carry;
+            misc[0] = nzb;
+            misc[1] = 0u;
+            misc[3] = 0u;
+        }
+    }
+    __syncthreads();
+    if (misc[0] == 1u) {
+        // one non-empty list: 0, 1, ..., n-1 (as yrss_scatter_lines)
+        const ListOut lo = list_out(P.qidx, P.n);
+        const uint32_t ph4 = ph & 3u;
+        const uint32_t head = min(P.n, (4u - ph4) & 3u);
+        const uint32_t nv = (P.n - head) >> 2;
+        const uint32_t T = gridDim.x * blockDim.x;
+        const uint32_t id = blockIdx.x * blockDim.x + t;
+        if (id < head)
+            list_store1<kListAux>(lo, id, id);
+        for (uint32_t v = id; v < nv; v += T) {
+            const uint32_t x = head + 4u * v;
+            list_store4<kListAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
+        }
+        const uint32_t e = head + 4u * nv + id;
+        if (e < P.n)
+            list_store1<kListAux>(lo, e, e);
+        return;
+    }
+    if (g0 >= g1)
+        return;
+    if (!P.early) {
+        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
+        load_span(g0, pk, qk);
+    }
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    if (t < nb) {
+        const uint32_t a = start[t] + pre0 + ph;
+        cs_sets[nb + t] = a;
+        ve_sets[nb + t] = a;
+    }
+    // Wave 0, a bucket to a lane, lays span g out into set s from set s ^ 1
+    // and the prefixes it holds: valid positions [cs, ve) = carried words and
+    // the span's packets, ce the first of the span's own; the list lines (an
+    // exclusive scan over buckets) and the stage index of each bucket's first
+    // packet (an exclusive scan of the span's counts); the table bias rb.
+    auto layout = [&](uint32_t g, uint32_t s) {
+        const uint32_t *pcs = cs_sets + (s ^ 1u) * nb, *pve = ve_sets + (s ^ 1u) * nb;
+        uint32_t *wcs = cs_sets + s * nb, *wve = ve_sets + s * nb, *wce = ce_sets + s * nb;
+        uint32_t *wsb = sb_sets + s * nb, *wrb = rb_sets + s * nb, *wlsl = lsl_sets + s * (nb + 1u);
+        uint32_t lines = 0, pk = 0;
+        const uint32_t ll = opaque(lane);
+#pragma unroll
+        for (uint32_t i = 0; i < kWideBI; ++i) {
+            if (i * kWave >= nb)   // (uniform)
+                break;
+            const uint32_t b = i * kWave + ll;
+            uint32_t nl = 0, v0 = 0, e0 = 0, cnt = 0, base = 0;
+            if (b < nb) {
+                // positions are start + prefix + ph: the span's first is the
+                // previous span's end, its end the prefix at its end chunk
+                e0 = pve[b];
+                v0 = max(pcs[b], e0 & ~15u);
+                base = start[b] + ph;
+                const uint32_t e1 = base + w0e[i];
+                cnt = e1 - e0;
+                wcs[b] = v0;
+                wce[b] = e0;
+                wve[b] = e1;
+                nl = ((e1 + 15u) >> 4) - (v0 >> 4);
+            }
+            const uint32_t x = wave_incl_scan(nl, lane);
+            const uint32_t y = wave_incl_scan(cnt, lane);
+            if (b < nb) {
+                wlsl[b] = lines + x - nl;
+                const uint32_t sbb = pk + y - cnt;
+                wsb[b] = sbb;
+                wrb[b] = sbb - (e0 - base);   // sb - prefix at the span's first chunk
+            }
+            lines += __shfl(x, kWave - 1, kWave);
+            pk += __shfl(y, kWave - 1, kWave);
+        }
+        if (lane == 0) {
+            const uint32_t len = span_end(g) - g * P.seg;
+            if (lines > P.lmax || pk != len) {
+                report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g, lines);
+                lines = 0;
+            }
+            wlsl[nb] = lines;
+            misc[4u + s] = lines;
+        }
+    };
+    __syncthreads();   // set 1 written
+    if (wave == 0)
+        layout(g0, 0u);
+    __syncthreads();
+    uint32_t wrote = 0, wsum = 0;
+    const uint32_t tk = kLineBlock / nb, tb = t % nb, tj = t / nb;
+    auto span = [&](uint32_t g, uint32_t s) {
+        const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
+        const bool last = g + 1u == g1;
+        const uint32_t *cs = cs_sets + s * nb, *ve = ve_sets + s * nb, *ce = ce_sets + s * nb;
+        const uint32_t *sb = sb_sets + s * nb, *rb = rb_sets + s * nb;
+        const uint32_t *lsl = lsl_sets + s * (nb + 1u);
+        const uint32_t *cbr = cb_sets + s * 16u * nb;           // carried into this span
+        uint32_t *cbw = cb_sets + (s ^ 1u) * 16u * nb;          // carried out of it
+        LPROF(0);
+        // (a) the prefix table with its rows' bias: stage index = tab + rank
+#pragma unroll
+        for (uint32_t k = 0; k < kWideTabRegs; ++k) {
+            const uint32_t e = k * kLineBlock + t;
+            if (k * kLineBlock < ntab && e < ntab)
+                tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k] + rb[e >> P.gshift];
+        }
+        __syncthreads();
+        LPROF(1);
+        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + s]);
+        // (b) the next span's loads; line tags; every packet's stage offset
+        if (!last)
+            load_span(g + 1u, pkn, qkn);
+        if (tj < tk) {
+            const uint32_t b = opaque(tb);
+            const uint32_t l0 = lsl[b], l1 = L ? min(lsl[b + 1u], L) : 0u, v0 = cs[b], e1 = ve[b];
+            for (uint32_t l = l0 + tj; l < l1; l += tk) {
+                const uint32_t gl = l - l0 + (v0 >> 4);
+                const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
+                                      : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
+                                                                                      : 2u;
+                ltag[l] = b | mode << 30;
+            }
+        }
+        auto place = [&](auto ragged) {
+            uint32_t slot[kWideG][8];
+#pragma unroll
+            for (uint32_t k = 0; k < kWideG; ++k) {
+                const uint32_t o8 = 8u * (k * kLineBlock + t);
+                const uint32_t cc = min(o8 >> P.cshift, ncs - 1u);
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j) {
+                    const uint32_t rk = (pk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu;
+                    const uint32_t b = bucket_of(
+                        (int16_t)((qk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu), P.nq);
+                    slot[k][j] = tab[__umul24(b, rs) + cc] + rk;
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kWideG; ++k) {
+                const uint32_t o8 = 8u * (k * kLineBlock + t);
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j)
+                    if (!decltype(ragged)::value || o8 + j < len)
+                        stg[min(slot[k][j], cap)] = (uint16_t)(o8 + j);
+            }
+        };
+        if (len == kWideSpan)
+            place(std::false_type{});
+        else
+            place(std::true_type{});
+        LPROF(2);
+        // the next span's streams and prefixes have arrived (waited before
+        // this span's list stores: vmcnt counts loads and stores in one
+        // queue); wave 0 lays the next span out before the barrier
+        __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        if (!last) {
+#pragma unroll
+            for (uint32_t k = 0; k < kWideG; ++k) {
+                pk[k] = pkn[k];
+                qk[k] = qkn[k];
+            }
+            if (wave == 0)
+                layout(g + 1u, s ^ 1u);
+        }
+        __syncthreads();
+        LPROF(3);
+        // the list word at adjusted position a of bucket b
+        auto word_at = [&](uint32_t b, uint32_t a, uint32_t csb, uint32_t ceb, uint32_t sbb) {
+            return a < ceb ? cbr[min(16u * b + (a - csb), 16u * nb - 1u)]
+                           : p0 + (uint32_t)stg[min(sbb + (a - ceb), cap)];
+        };
+        // (c) copy-out: whole quads of whole and partial lines as 16-byte
+        // stores; carried lines (mode 1) wait for the next span
+        auto copy_quad = [&](uint32_t v, uint32_t tag) {
+            const uint32_t mode = tag >> 30;
+            if (mode == 1u)
+                return;
+            const uint32_t b = tag & 0xffffu;
+            const uint32_t v0 = cs[b], e1 = ve[b], e0 = ce[b], sbb = sb[b];
+            const uint32_t gl = (v >> 2) - lsl[b] + (v0 >> 4);
+            const uint32_t a0 = 16u * gl + 4u * (v & 3u);
+            if (mode == 2u && !(a0 >= v0 && a0 + 4u <= e1))
+                return;   // a cut quad: the pass below
+            const u32x4 e{word_at(b, a0, v0, e0, sbb), word_at(b, a0 + 1u, v0, e0, sbb),
+                          word_at(b, a0 + 2u, v0, e0, sbb), word_at(b, a0 + 3u, v0, e0, sbb)};
+            const uint32_t d = a0 - ph;
+            if (d + 4u <= P.n && d + 4u > d) {
+                list_store4<kListAuxMany>(lout, d, e);
+                wrote += 4u;
+                wsum += e.x + e.y + e.z + e.w;
+            } else {
+                report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
+            }
+        };
+        constexpr uint32_t kCopyQ = 2u;
+        for (uint32_t v0 = t; v0 < 4u * L; v0 += kCopyQ * kLineBlock) {
+            uint32_t tg[kCopyQ];
+#pragma unroll
+            for (uint32_t i = 0; i < kCopyQ; ++i) {
+                const uint32_t v = v0 + i * kLineBlock;
+                tg[i] = v < 4u * L ? ltag[v >> 2] : 1u << 30;
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kCopyQ; ++i)
+                copy_quad(v0 + i * kLineBlock, tg[i]);
+        }
+        // the cut quads of partial lines, a thread per (bucket, quad, word)
+        for (uint32_t e = t; e < 8u * nb; e += kLineBlock) {
+            const uint32_t b = e >> 3, k = (e >> 2) & 1u, j = e & 3u;
+            const uint32_t v0 = cs[b], e1 = ve[b];
+            const uint32_t qb = (k ? e1 : v0) & ~3u, a = qb + j;
+            bool go = a >= v0 && a < e1 && ((k ? e1 : v0) & 3u) != 0u;
+            if (k == 0u)
+                go = go && !(!last && (v0 >> 4) == (e1 >> 4) && (e1 & 15u) != 0u);
+            else
+                go = go && last && !(qb == (v0 & ~3u) && (v0 & 3u) != 0u);
+            if (go) {
+                const uint32_t w = word_at(b, a, v0, ce[b], sb[b]), d = a - ph;
+                if (d < P.n) {
+                    list_store1<kListAuxMany>(lout, d, w);
+                    ++wrote;
+                    wsum += w;
+                } else {
+                    report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
+                }
+            }
+        }
+        LPROF(4);
+        // (d) carry the unfinished last lines into the other set
+        if (!last) {
+            for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
+                const uint32_t b = e >> 4, j = e & 15u;
+                const uint32_t e1 = ve[b], v0 = cs[b], nv = max(v0, e1 & ~15u);
+                if (j < e1 - nv)
+                    cbw[e] = word_at(b, nv + j, v0, ce[b], sb[b]);
+            }
+        }
+        LPROF(5);
+    };
+    for (uint32_t g = g0; g < g1; ++g)
+        span(g, (g - g0) & 1u);
+    wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
+    wsum = __shfl(wave_incl_scan(wsum, lane), kWave - 1, kWave);
+    if (lane == 0) {
+        atomicAdd(&misc[3], wrote);
+        atomicAdd(&misc[1], wsum);
+    }
+    __syncthreads();
+    if (t == 0) {
+        const uint64_t a = (uint64_t)g0 * P.seg, e = span_end(g1 - 1u);
+        const uint32_t want = (uint32_t)(e - a);
+        const uint32_t want_sum = (uint32_t)((e - a) * (a + e - 1u) / 2u);
+        if (misc[3] != want)
+            report_fault(P.fault, YRSS_FAULT_COUNT_MISMATCH, YRSS_K_SCATTER, g0, misc[3]);
+        else if (misc[1] != want_sum)
+            report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g0, misc[1]);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // ff_rss_check (ff_dpdk_if.c:1904-1940) in batch: the connect-side RSS check
 // F-Stack runs per candidate lport in in_pcbconnect_setup (in_pcb.c:1131-1170).
 // The tuple is hashed in its raw stored (network-order) byte order, unlike
@@ -2884,7 +3315,8 @@ ScatterLds scatter_lds(uint32_t nb)
 // than a span can be (batches past ~2^29 packets) or the LDS would not fit.
 struct LinePlan {
     bool ok, packed;
-    bool fits;   // nb within the kernel's per-bucket capacity (line_nb_max)
+    bool fits;   // nb within the kernel's per-bucket capacity (line_nb_max, kWideNbMax)
+    bool wide;   // yrss_scatter_wide (past 128 buckets), else yrss_scatter_lines<kG>
     uint32_t groups, gshift, seg, lmax, lds;
 };
 
@@ -2892,28 +3324,33 @@ LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
 {
     LinePlan p{};
     const uint32_t nb = c->nb, cshift = lay.ct_shift + 6u;
-    p.groups = nb > line_nb_max(2) ? 4u : 2u;
-    if (c->dbg.line_groups)   // test builds only (yrss_debug_line_groups)
-        p.groups = c->dbg.line_groups;
-    p.fits = nb <= line_nb_max(p.groups) && nb <= (uint32_t)kLineBlock;
-    const uint32_t smax = line_span_max(p.groups);
+    // past 128 buckets the wide kernel (two workgroups a CU); the test hook
+    // forces a kernel: 1 wide, 2 / 4 yrss_scatter_lines<kG>
+    const uint32_t force = c->dbg.line_groups;
+    p.wide = force ? force == 1u : nb > line_nb_max(2);
+    p.groups = p.wide ? kWideG : force ? force : 2u;
+    p.fits = (p.wide ? nb <= kWideNbMax : nb <= line_nb_max(p.groups)) &&
+             nb <= (uint32_t)kLineBlock;
+    const uint32_t smax = p.wide ? kWideSpan : line_span_max(p.groups);
+    const uint32_t tmax = p.wide ? kWideTabMax : line_tab_max(p.groups);
     if (lay.chunk > smax || nb > (uint32_t)kLineBlock)
         return p;
     uint64_t target = c->tune.span_tiles ? (uint64_t)c->tune.span_tiles * kTile : smax;
     target = std::min<uint64_t>(std::max<uint64_t>(target, lay.chunk), smax);
     p.gshift = 0;
     while (((uint64_t)lay.chunk << (p.gshift + 1)) <= target &&
-           ((uint64_t)nb << (p.gshift + 1)) <= line_tab_max(p.groups))
+           ((uint64_t)nb << (p.gshift + 1)) <= tmax)
         ++p.gshift;
-    if (((uint64_t)nb << p.gshift) > line_tab_max(p.groups))
+    if (((uint64_t)nb << p.gshift) > tmax)
         return p;
     p.seg = lay.chunk << p.gshift;
     p.lmax = p.seg / 16u + 2u * nb + 1u;   // a bucket's lines <= (its packets + 30) / 16
-    p.lds = line_lds(nb, p.gshift, p.lmax).words * 4u;
+    p.lds = (p.wide ? wide_lds(nb, p.gshift, p.lmax, p.seg).words
+                    : line_lds(nb, p.gshift, p.lmax).words) * 4u;
     if (p.lds > 160u * 1024u)
         return p;
-    // bucket << cshift | rank fits 16 bits
-    p.packed = cshift < 16u && nb <= (1u << (16u - cshift));
+    // bucket << cshift | rank fits 16 bits (the wide kernel always reads q)
+    p.packed = !p.wide && cshift < 16u && nb <= (1u << (16u - cshift));
     p.ok = true;
     return p;
 }
@@ -3792,8 +4229,9 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         // spans, never more workgroups than spans
         const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
         void (*fn)(LineParams) =
-            lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
-                            : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
+            lp.wide ? yrss_scatter_wide
+            : lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
+                              : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
         const uint32_t sgrid =
             std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
         Timed t(c, YRSS_K_SCATTER);
@@ -4870,7 +5308,7 @@ int yrss_debug_worker_inject(yrss_ctx *c, uint64_t ticket)
 
 int yrss_debug_line_groups(yrss_ctx *c, uint32_t groups, int skip_host_check)
 {
-    if (!c || (groups != 0u && groups != 2u && groups != 4u) || skip_host_check < 0 ||
+    if (!c || groups > 4u || groups == 3u || skip_host_check < 0 ||
         skip_host_check > 1)
         return -EINVAL;
     c->dbg.line_groups = groups;
