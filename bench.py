@@ -84,6 +84,9 @@ def parse_args(argv=None):
                     help="after the headline, each rank also classifies a --pkts shard of "
                          "these profiles (BASELINE configs[3], configs[4]: the 8-GPU "
                          "configs), reported under configs_extra, never as value ('' = off)")
+    ap.add_argument("--test-hooks", default="",
+                    help="measurements only: run libyrss_test.so with its yrss_debug_* hooks, "
+                         "k=v[,k=v] (merge, groups, desync); the line says so")
     ap.add_argument("--dry", action="store_true",
                     help="plumbing check without a GPU (rank spawn, barrier, reductions); "
                          "prints a line marked dry, never a measurement")
@@ -812,8 +815,16 @@ def main(argv=None):
     torch.cuda.set_device(local)
     devices = check_devices(device_identity(local, False), world)
     nbq = args.nb_queues or args.nb_procs
+    hooks = {k: int(v) for k, v in (kv.split("=") for kv in args.test_hooks.split(",") if kv)}
     eng = SoftRss(nb_procs=args.nb_procs, nb_queues=nbq, soft_dispatch=1,
-                  dispatch_only_core=args.dispatch_only_core, device=local, max_burst=0)
+                  dispatch_only_core=args.dispatch_only_core, device=local, max_burst=0,
+                  lib_path=str(abi.TEST_LIB_PATH) if hooks else None)
+    if "merge" in hooks:
+        abi.check(eng._lib.yrss_debug_partial_merge(eng._ctx, hooks["merge"]), "partial_merge")
+    if "groups" in hooks:
+        abi.check(eng._lib.yrss_debug_line_groups(eng._ctx, hooks["groups"], 0), "line_groups")
+    if "desync" in hooks:
+        abi.check(eng._lib.yrss_debug_line_desync(eng._ctx, hooks["desync"]), "line_desync")
     if args.tune:
         eng.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
     n = args.pkts
@@ -967,6 +978,7 @@ def main(argv=None):
                 "dispatch_only_core": args.dispatch_only_core,
                 "per_queue_lists": not args.no_compact,
                 "kni_filter": args.filter,
+                "test_hooks": hooks or None,
                 "parallelism": f"shard{world}",
                 "devices": devices,
             },

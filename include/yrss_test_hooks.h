@@ -30,6 +30,17 @@ int yrss_debug_worker_inject(yrss_ctx *ctx, uint64_t ticket);
  * the kernel's entry check must report YRSS_FAULT_LINE_CAPACITY and leave. */
 int yrss_debug_line_groups(yrss_ctx *ctx, uint32_t groups, int skip_host_check);
 
+/* Odd line-scatter workgroups wait this many 100 MHz ticks (<= 100000)
+ * before starting: a measurement of what the workgroups' lockstep costs
+ * (results unchanged).  0 disables. */
+int yrss_debug_line_desync(yrss_ctx *ctx, uint32_t ticks);
+
+/* 1: the partial list lines of a workgroup's range (its first and last line
+ * of each bucket, the other part written by the neighbouring range) leave as
+ * plain stores, so the two parts can meet in L2 and be written back once;
+ * 0: streaming stores like every other line (results unchanged). */
+int yrss_debug_partial_merge(yrss_ctx *ctx, int on);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,7 +50,11 @@ def main() -> int:
     for s in args.libs.split(","):
         path, _, tune = s.partition("@")
         tune = tune or args.tune
-        specs.append((s, None if path == "cur" else str(ROOT / path),
+        # "test": libyrss_test.so, whose hooks the dbg_* keys drive
+        # (dbg_groups: yrss_debug_line_groups, dbg_desync: yrss_debug_line_desync)
+        lib = None if path == "cur" else str(abi.TEST_LIB_PATH) if path == "test" \
+            else str(ROOT / path)
+        specs.append((s, lib,
                       {k: int(v) for k, v in (kv.split("=") for kv in tune.split(";") if kv)}
                       if tune else {}))
     rng = random.Random(args.seed)
@@ -70,6 +74,13 @@ def main() -> int:
                 tn = dict(tune)
                 # side=1: the caller's work on a non-default (non-blocking) stream
                 st = torch.cuda.Stream() if tn.pop("side", 0) else None
+                grp, des = tn.pop("dbg_groups", 0), tn.pop("dbg_desync", 0)
+                if tn.pop("dbg_merge", 0):
+                    assert e._lib.yrss_debug_partial_merge(e._ctx, 1) == 0
+                if grp:
+                    assert e._lib.yrss_debug_line_groups(e._ctx, grp, 0) == 0
+                if des:
+                    assert e._lib.yrss_debug_line_desync(e._ctx, des) == 0
                 if tn:
                     e.set_tuning(**tn)
                 wins = [e.synth(PROFILES[args.profile], n, k * n, stride=stride)

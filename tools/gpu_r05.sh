@@ -43,7 +43,66 @@ wide1)
     step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-3,64,129,255}" \
         --libs "cur,ablib/libyrss_r05base.so" --rounds "${AB_ROUNDS:-6}" || exit 1
     step winab 600 python tools/win_ab.py || exit 1
-    cat gpurun_out/ab.log gpurun_out/winab.log
+    # write bytes: the bare list-write pattern, then the scatter at 255 queues
+    for nb in 64 256; do
+        timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_lw$nb -o run \
+            --output-format csv -- tools/list_write_bw 16777216 $nb 8192 2 2 5 \
+            > gpurun_out/pmc_lw$nb.log 2>&1 || { echo "pmc lw rc=$?"; exit 1; }
+        python tools/pmc_kernels.py gpurun_out/pmc_lw$nb > gpurun_out/pmc_lw$nb.sum 2>&1
+    done
+    B="--profile tcp4 --nb-procs 255 --steps 5 --warmup 2 --cpu-seconds 0 --pcie 0 --check 0 --extra-configs="
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_w255 -o run --output-format csv \
+        -- python bench.py $B > gpurun_out/pmc_w255.log 2>&1 || { echo "pmc w255 rc=$?"; exit 1; }
+    python tools/pmc_kernels.py gpurun_out/pmc_w255 > gpurun_out/pmc_w255.sum 2>&1
+    cat gpurun_out/ab.log gpurun_out/winab.log gpurun_out/pmc_lw*.sum gpurun_out/pmc_w255.sum
+    ;;
+wide2)
+    step tests_wide 400 python -u -m pytest tests/test_gpu_layout.py -x -q --timeout 120 \
+        --timeout-method thread -k "wide or forced_line or capacity or bucket_counts or xcd" || exit 1
+    step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-129,255}" \
+        --libs "test,test@dbg_groups=1" --rounds "${AB_ROUNDS:-4}" || exit 1
+    tools/build_ab_lib.sh prof -DYRSS_PROF_LINES=1 -DYRSS_TEST_HOOKS=1 > gpurun_out/build_prof.log 2>&1 || exit 1
+    step lineprof 200 python tools/line_prof.py --lib ab/lib/libyrss_prof.so --nb-procs 129,255 --pipe --groups 1 || exit 1
+    cat gpurun_out/ab.log gpurun_out/lineprof.log
+    ;;
+skel)
+    : > gpurun_out/skel.log
+    for cfg in "4 16384 1" "64 8192 2" "256 16384 1" "256 8192 2"; do
+        set -- $cfg
+        for rd in 0 1 2; do
+            timeout -k 5 60 tools/list_write_bw 16777216 $1 $2 $3 2 20 $rd >> gpurun_out/skel.log 2>&1 \
+                || { echo "skel rc=$?"; exit 1; }
+        done
+    done
+    cat gpurun_out/skel.log
+    step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-8,64,255}" \
+        --libs "test,test@dbg_merge=1" --rounds "${AB_ROUNDS:-4}" || exit 1
+    cat gpurun_out/ab.log
+    for m in 0 1; do
+        for q in 64 255; do
+            B="--profile tcp4 --nb-procs $q --steps 5 --warmup 2 --cpu-seconds 0 --pcie 0 --check 0 --extra-configs= --test-hooks merge=$m"
+            timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_m${m}_$q -o run --output-format csv \
+                -- python bench.py $B > gpurun_out/pmc_m${m}_$q.log 2>&1 || { echo "pmc rc=$?"; exit 1; }
+            echo "== merge $m q$q"; python tools/pmc_kernels.py gpurun_out/pmc_m${m}_$q | grep -A2 scatter
+        done
+    done
+    ;;
+desync)
+    L="test@dbg_groups=4,test@dbg_groups=4;dbg_desync=250,test@dbg_groups=4;dbg_desync=500"
+    L="$L,test@dbg_groups=1,test@dbg_groups=1;dbg_desync=300"
+    step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-255,129}" --libs "$L" \
+        --rounds "${AB_ROUNDS:-4}" || exit 1
+    cat gpurun_out/ab.log
+    ;;
+prof)
+    # the line scatter's phase clock (a tools build with the test hooks)
+    tools/build_ab_lib.sh prof -DYRSS_PROF_LINES=1 -DYRSS_TEST_HOOKS=1 > gpurun_out/build_prof.log 2>&1 || exit 1
+    : > gpurun_out/lineprof.log
+    for g in ${PROF_GROUPS:-0 4}; do
+        timeout -k 10 200 python tools/line_prof.py --lib ab/lib/libyrss_prof.so \
+            --nb-procs "${PROF_Q:-64,128,255}" --groups $g >> gpurun_out/lineprof.log 2>&1 || exit 1
+    done
+    cat gpurun_out/lineprof.log
     ;;
 ab)
     step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-3,64,255}" --libs "${AB_LIBS}" \

@@ -24,6 +24,8 @@ import torch  # noqa: E402
 from yastack_amd import SoftRss, abi  # noqa: E402
 
 PH = ["a tab + layout + S1", "b tags/carried/place", "wait + S2", "c copy-out", "d carry"]
+# yrss_scatter_wide (the pipelined kernel past 128 buckets): stamps per phase
+PH_PIPE = ["loads + copy-out c-1", "tags + place c", "wait", "layout + tab c+1", "barrier"]
 
 
 def main() -> int:
@@ -31,13 +33,23 @@ def main() -> int:
     ap.add_argument("--lib", required=True)
     ap.add_argument("--nb-procs", default="8,64")
     ap.add_argument("--pkts", type=int, default=1 << 24)
+    ap.add_argument("--groups", type=int, default=0,
+                    help="force the line-scatter kernel (yrss_debug_line_groups: 1 wide, 2 / 4 "
+                         "kG); needs a -DYRSS_TEST_HOOKS build")
+    ap.add_argument("--pipe", action="store_true",
+                    help="phase names of the pipelined wide kernel (past 128 buckets)")
     args = ap.parse_args()
+    global PH
+    if args.pipe:
+        PH = PH_PIPE
     lib = abi.load(str(ROOT / args.lib))
     lib.yrss_debug_line_prof.restype = ctypes.c_int
     lib.yrss_debug_line_prof.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     n = args.pkts
     for npr in (int(x) for x in args.nb_procs.split(",")):
         e = SoftRss(npr, npr, 1, 1, device=0, max_burst=0, lib_path=str(ROOT / args.lib))
+        if args.groups:
+            assert e._lib.yrss_debug_line_groups(e._ctx, args.groups, 0) == 0
         w, l = e.synth(abi.SYN_TCP4, n, 0)
         out = e.alloc_out(n, w.device)
         buf = np.zeros(2048 * 8 * 8, np.uint64)
@@ -58,7 +70,7 @@ def main() -> int:
             print(f"q{npr}: no spans (one-list batch)")
             e.close()
             continue
-        print(f"q{npr}: {blocks} workgroups, spans per workgroup {spans.min()}-{spans.max()}")
+        print(f"q{npr} groups {args.groups}: {blocks} workgroups, spans per workgroup {spans.min()}-{spans.max()}")
         for k, name in enumerate(PH):
             v = d[:, :, k][m[:, :, k]]
             if v.size == 0:

@@ -10,6 +10,10 @@
 //     SPAN    packets per span (8192, 16384)
 //     WG_PER_CU  1 or 2: resident 512-thread workgroups per CU (LDS padding)
 //     AUX     store cache policy: 2 nt (past 64 buckets), 18 nt|sc1, 0 plain
+//     RD      0: writes only; 1: each span first reads 4 B a packet (two
+//             16-bit streams, as the scatter's rank and q at > 128 buckets),
+//             waits, then writes; 2: span g + 1's reads issued before span
+//             g's writes (one span of look-ahead)
 // Prints one JSON line: kernel us (mean of REPS), GB/s of list bytes.
 #include <hip/hip_runtime.h>
 
@@ -22,8 +26,9 @@
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kRsrcWord3 = 0x00020000;
 
-template <int kAux>
-__global__ __launch_bounds__(512) void list_writes(uint32_t *lists, uint32_t n, uint32_t nb,
+template <int kAux, int kRd>
+__global__ __launch_bounds__(512) void list_writes(uint32_t *lists, const uint16_t *ra,
+                                                   const uint16_t *qa, uint32_t n, uint32_t nb,
                                                    uint32_t span, uint32_t xcd)
 {
     extern __shared__ uint32_t pad[];
@@ -41,11 +46,41 @@ __global__ __launch_bounds__(512) void list_writes(uint32_t *lists, uint32_t n, 
                                                                         kRsrcWord3);
     if (t == 0)
         pad[0] = g0;   // keep the LDS allocation
+    // the span's streams: span / 512 packets a thread, 16 bytes = 8 packets a load
+    const uint32_t per = span / 512u / 8u;   // loads a thread per stream (<= 8)
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(ra), 0, (int)(n * 2u), kRsrcWord3);
+    const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t *>(qa), 0, (int)(n * 2u), kRsrcWord3);
+    u32x4 a[8], b[8];
+    uint32_t acc = 0;
+    auto load = [&](uint32_t g) {
+#pragma unroll
+        for (uint32_t k = 0; k < 8u; ++k)
+            if (k < per) {
+                const int off = (int)((g * span + 8u * (k * 512u + t)) * 2u);
+                a[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 2));
+                b[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rq, off, 0, 2));
+            }
+    };
+    if (kRd == 2 && g0 < g1)
+        load(g0);
     for (uint32_t g = g0; g < g1; ++g) {
+        if (kRd == 1)
+            load(g);
+        if (kRd) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+#pragma unroll
+            for (uint32_t k = 0; k < 8u; ++k)
+                if (k < per)
+                    acc += a[k].x ^ b[k].w;
+        }
+        if (kRd == 2 && g + 1u < g1)
+            load(g + 1u);
         for (uint32_t v = t; v < span / 4u; v += 512u) {
             const uint32_t b = v / qpr, k = v - b * qpr;
             const uint32_t d = b * len + g * run + 4u * k;
-            const uint32_t x = g * span + 4u * v;
+            const uint32_t x = g * span + 4u * v + (acc & 0x80000000u);   // (keep the loads)
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{x, x + 1u, x + 2u, x + 3u}, rs,
                                                    (int)(d * 4u), 0, kAux);
         }
@@ -63,7 +98,9 @@ int main(int argc, char **argv)
     const uint32_t span = (uint32_t)strtoul(argv[3], 0, 0), wpc = (uint32_t)strtoul(argv[4], 0, 0);
     const int aux = argc > 5 ? atoi(argv[5]) : 2;
     const int reps = argc > 6 ? atoi(argv[6]) : 20;
-    if (!n || !nb || !span || n % span || span % (16u * nb) || (wpc != 1 && wpc != 2)) {
+    const int rd = argc > 7 ? atoi(argv[7]) : 0;
+    if (!n || !nb || !span || n % span || span % (16u * nb) || (wpc != 1 && wpc != 2) ||
+        span > 32768u || span % 4096u || rd < 0 || rd > 2) {
         fprintf(stderr, "bad shape\n");
         return 2;
     }
@@ -71,18 +108,27 @@ int main(int argc, char **argv)
     if (hipGetDeviceProperties(&p, 0) != hipSuccess)
         return 1;
     uint32_t *lists = nullptr;
-    if (hipMalloc((void **)&lists, (size_t)n * 4u) != hipSuccess)
+    uint16_t *ra = nullptr, *qa = nullptr;
+    if (hipMalloc((void **)&lists, (size_t)n * 4u) != hipSuccess ||
+        hipMalloc((void **)&ra, (size_t)n * 2u) != hipSuccess ||
+        hipMalloc((void **)&qa, (size_t)n * 2u) != hipSuccess)
+        return 1;
+    if (hipMemset(ra, 0, (size_t)n * 2u) != hipSuccess || hipMemset(qa, 0, (size_t)n * 2u) != hipSuccess)
         return 1;
     const uint32_t cus = (uint32_t)p.multiProcessorCount;
     const uint32_t grid = std::min<uint32_t>(cus * wpc, n / span);
     const size_t lds = wpc == 1 ? 100u * 1024u : 70u * 1024u;   // 1 or 2 resident per CU
     auto launch = [&](hipStream_t s) {
-        if (aux == 18)
-            hipLaunchKernelGGL(list_writes<18>, dim3(grid), dim3(512), lds, s, lists, n, nb, span, 1u);
-        else if (aux == 0)
-            hipLaunchKernelGGL(list_writes<0>, dim3(grid), dim3(512), lds, s, lists, n, nb, span, 1u);
-        else
-            hipLaunchKernelGGL(list_writes<2>, dim3(grid), dim3(512), lds, s, lists, n, nb, span, 1u);
+#define LW(A, R) hipLaunchKernelGGL((list_writes<A, R>), dim3(grid), dim3(512), lds, s, lists, ra, qa, n, \
+                                     nb, span, 1u)
+        if (aux == 18) {
+            if (rd == 0) LW(18, 0); else if (rd == 1) LW(18, 1); else LW(18, 2);
+        } else if (aux == 0) {
+            if (rd == 0) LW(0, 0); else if (rd == 1) LW(0, 1); else LW(0, 2);
+        } else {
+            if (rd == 0) LW(2, 0); else if (rd == 1) LW(2, 1); else LW(2, 2);
+        }
+#undef LW
     };
     for (int i = 0; i < 3; ++i)
         launch(0);
@@ -108,9 +154,12 @@ int main(int argc, char **argv)
     const bool ok = sum == (uint64_t)n * (n - 1u) / 2u;
     const double us = total / reps * 1e3;
     printf("{\"tool\": \"list_write_bw\", \"n\": %u, \"nb\": %u, \"span\": %u, \"wg_per_cu\": %u, "
-           "\"grid\": %u, \"aux\": %d, \"us\": %.2f, \"GBps\": %.1f, \"sum_ok\": %s}\n",
-           n, nb, span, wpc, grid, aux, us, (double)n * 4.0 / us / 1e3, ok ? "true" : "false");
+           "\"grid\": %u, \"aux\": %d, \"rd\": %d, \"us\": %.2f, \"GBps\": %.1f, \"sum_ok\": %s}\n",
+           n, nb, span, wpc, grid, aux, rd, us, (double)n * (rd ? 8.0 : 4.0) / us / 1e3,
+           ok ? "true" : "false");
     free(h);
     (void)hipFree(lists);
+    (void)hipFree(ra);
+    (void)hipFree(qa);
     return ok ? 0 : 1;
 }

@@ -15,7 +15,8 @@ from collections import defaultdict
 
 def short(name):
     name = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
-    for k in ("yrss_parse_hash", "yrss_seg_scan", "yrss_scatter_lines", "yrss_scatter",
+    for k in ("yrss_parse_hash", "yrss_seg_scan", "yrss_scatter_lines", "yrss_scatter_wide",
+              "yrss_scatter", "list_writes",
               "yrss_synth", "probe"):
         if k in name:
             return k + ("<" + name.split("<", 1)[1].split(">")[0] + ">" if "<" in name else "")
@@ -34,7 +35,7 @@ def main():
             for (_, k, c), v in per.items():
                 vals[k][c].append(v)
     for k in sorted(vals):
-        if not any(s in k for s in ("parse", "scan", "scatter")):
+        if not any(s in k for s in ("parse", "scan", "scatter", "list_writes")):
             continue
         c = {n: sum(v) / len(v) for n, v in vals[k].items()}
         print(f"  {k}")

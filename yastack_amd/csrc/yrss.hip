@@ -1243,6 +1243,8 @@ struct LineParams {
     uint32_t xcd;              // workgroups of one XCD take consecutive ranges
     uint32_t nt;               // list stores non-temporal only (no sc1): past 64 buckets
     uint32_t early;            // first span's loads before the totals: past 16 buckets
+    uint32_t desync;           // test builds only: odd workgroups start this many 100 MHz ticks late
+    uint32_t merge;            // partial lines (a range's first / last) as plain stores: L2 merges
 };
 
 // LDS of a workgroup, in words: per-bucket arrays, the prefix table, the
@@ -1326,6 +1328,22 @@ __device__ uint64_t g_line_prof[2048 * 8 * 8];
     } while (0)
 #endif
 
+// Test builds only (yrss_debug_line_desync): odd workgroups start late, so
+// that neighbouring workgroups' read and write phases interleave instead of
+// running in lockstep (a measurement of the lockstep's cost)
+__device__ __forceinline__ void line_desync(uint32_t ticks)
+{
+#ifdef YRSS_TEST_HOOKS
+    if (ticks && (blockIdx.x & 1u)) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < ticks)
+            __builtin_amdgcn_s_sleep(8);
+    }
+#else
+    (void)ticks;
+#endif
+}
+
 template <bool kPacked, uint32_t kG>
 __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lines(LineParams P)
 {
@@ -1340,6 +1358,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             report_fault(P.fault, YRSS_FAULT_LINE_CAPACITY, YRSS_K_SCATTER, nb, line_nb_max(kG));
         return;
     }
+    line_desync(P.desync);
     const LineLds o = line_lds(nb, P.gshift, P.lmax);
 #ifdef YRSS_PROF_LINES
     if (t == 0 && blockIdx.x < 2048u)   // kernel entry, slot 7 of span 0
@@ -1703,7 +1722,9 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 if (a0 >= v0 && a0 + 4u <= e1) {
                     const uint32_t d = a0 - ph;
                     if (d + 4u <= P.n && d + 4u > d) {
-                        if (P.nt)
+                        if (P.merge)   // plain: the line's other part meets it in L2
+                            list_store4<0>(lout, d, e);
+                        else if (P.nt)
                             list_store4<kListAuxMany>(lout, d, e);
                         else
                             list_store4<kListAux>(lout, d, e);
@@ -1764,7 +1785,9 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             if (go) {
                 const uint32_t w = stg[min(so[b] + a, cap)], d = a - ph;
                 if (d < P.n) {
-                    if (P.nt)
+                    if (P.merge)
+                        list_store1<0>(lout, d, w);
+                    else if (P.nt)
                         list_store1<kListAuxMany>(lout, d, w);
                     else
                         list_store1<kListAux>(lout, d, w);
@@ -1814,40 +1837,58 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
 }
 
 // ---------------------------------------------------------------------------
-// Kernel 3 (ranked, many buckets): the lists in whole lines at two workgroups
-// per CU (round 5).  Past 128 buckets the line scatter above needs 16 384-
-// packet spans to amortise its per-bucket work, and its stage of 32-bit words
-// laid out line for line (two lines of padding a bucket) then holds 145 KB of
-// LDS: one workgroup per CU, whose copy-out (the chip's list writes) and
-// placement (LDS) cannot overlap another's.  The list writes alone take
-// 13-15 us for 2^24 packets at any bucket count (tools/list_write_bw.hip,
-// profiles/r05_list_write_bw.log), against 52 us for the kernel at 256: the
-// phases, not the store pattern, are the cost.  This kernel fits 8192-packet
-// spans of up to 320 buckets in <= 80 KB:
-// - the stage is compact and 16-bit: the span's packets sorted by bucket as
-//   offsets from the span's first packet (8192 x 2 bytes), no line padding;
-//   bucket b's packets start at stage index sb[b] (an exclusive scan of the
-//   span's counts), a packet's index is tab[b][chunk] + rank as before;
-// - the words carried from earlier spans (a bucket's unfinished last line,
-//   <= 15 words) stay 32-bit in a carry array of two sets, one read by this
-//   span's copy-out and one written for the next, so the carry needs no
-//   barrier of its own;
-// - a list word at adjusted position a of bucket b is the carried word
-//   cb[b][a - cs[b]] below ce[b], else p0 + stage[sb[b] + a - ce[b]];
-// - wave 0 lays the next span out right after its own placement, before the
-//   copy-out barrier, so a span takes two barriers.
-// Same outputs, checks and fault records as yrss_scatter_lines; always reads
-// the rank beside q (no 16-bit packing past 64 buckets at these chunks).
+// Kernel 3 (ranked, many buckets): the lists in whole lines, software-
+// pipelined (round 5).
+//
+// Past 128 buckets yrss_scatter_lines runs 16 384-packet spans at one
+// workgroup per CU (145 KB of LDS), and its phase clock at 256 buckets shows
+// what a span costs (profiles/r05_lineprof_wide1.log): every workgroup runs
+// the same schedule, so the chip reads the next span's streams in one phase
+// (placement + wait, 4.4 us) and writes the lists in another (copy-out,
+// 5.5 us), with LDS-only phases (tags, carry, layout) between them, while the
+// list writes alone take 13-15 us for 2^24 packets at any bucket count
+// (tools/list_write_bw.hip, profiles/r05_list_write_bw.log).  Two workgroups
+// a CU in 80 KB (8192-packet spans) did not help: they run in the same
+// lockstep (r05 A/B: scatter 57.6 against 53.0 us at 256 buckets).
+//
+// Here a 1024-thread workgroup splits its waves: in one phase waves 0-7
+// issue span c + 1's loads, tag and place span c into one stage, wait for the
+// loads, lay span c + 1 out and write its prefix table, while waves 8-15 copy
+// span c - 1 out of the other stage and carry its unfinished lines; both meet
+// at the phase's only barrier.  A wave stalled on its stores (the chip's list
+// writes) no longer holds up the placement behind it in program order, and
+// the copy-out waves' stores do not sit in the placement waves' vmcnt queue.
+// (One 512-thread group doing both in turn, the first form of this kernel,
+// was slower: its stores stalled it before it could place.)  So the
+// stage, the line tags and the prefix table come in two buffers, the
+// per-bucket layout in three sets (span c - 1's copy-out, span c's tags and
+// placement, span c + 1's layout), the carried words in two.
+// - The stage is compact and 16-bit: a span's packets sorted by bucket as
+//   offsets from the span's first packet (no line padding); a packet's stage
+//   index is tab[b][chunk] + rb[b] + rank with tab the raw prefixes.
+// - The words carried from earlier spans (a bucket's unfinished last line,
+//   <= 15) stay 32-bit: a list word at adjusted position a of bucket b is
+//   cb[b][a - cs[b]] below ce[b], else p0 + stage[sb[b] + a - ce[b]].
+// - Each list line is tagged with its bucket, flags and the stage index of
+//   its first position, so a whole line's quad is two LDS reads and four
+//   stage halfwords.
+// Same outputs, checks and fault records as yrss_scatter_lines; it always
+// reads the rank beside q (the bucket does not pack beside it at these
+// chunks).
 // ---------------------------------------------------------------------------
-constexpr uint32_t kWideG = 2;                             // 8-packet groups a thread
-constexpr uint32_t kWideSpan = kLineBlock * 8u * kWideG;   // 8192 packets
+constexpr uint32_t kWideG = 4;                             // 8-packet groups a thread
+constexpr uint32_t kWideSpan = kLineBlock * 8u * kWideG;   // 16384 packets
 constexpr uint32_t kWideBI = 5;                            // buckets a wave-0 lane holds
 constexpr uint32_t kWideNbMax = 64u * kWideBI;             // 320 (nb <= 257 in use)
 constexpr uint32_t kWideTabRegs = 5;                       // nb x span chunks <= 2560
 constexpr uint32_t kWideTabMax = kLineBlock * kWideTabRegs;
+// line tag: bucket in the low 16 bits and
+constexpr uint32_t kTagSkip = 1u << 31;      // carried to the next span, not stored now
+constexpr uint32_t kTagPartial = 1u << 30;   // a range's first / last line: cut quads by the pass
+constexpr uint32_t kTagCarried = 1u << 29;   // holds carried words: read through word_at
 
 struct WideLds {
-    uint32_t start, cs, ve, ce, sb, rb, lsl, misc, tab, cb, ltag, stg, words;
+    uint32_t start, cs, ve, ce, sb, rb, lsl, misc, tab, cb, ltag, lsrc, stg, stg_words, words;
 };
 __host__ __device__ inline WideLds wide_lds(uint32_t nb, uint32_t gshift, uint32_t lmax,
                                             uint32_t seg)
@@ -1860,50 +1901,55 @@ __host__ __device__ inline WideLds wide_lds(uint32_t nb, uint32_t gshift, uint32
         return at;
     };
     L.start = take(nb);
-    L.cs = take(2u * nb);    // first valid adjusted position (carried words first)
-    L.ve = take(2u * nb);    // end adjusted position
-    L.ce = take(2u * nb);    // first position of the span's own packets
-    L.sb = take(2u * nb);    // stage index of the bucket's first packet
-    L.rb = take(2u * nb);    // prefix table row bias (to stage indices)
-    L.lsl = take(2u * (nb + 1u));   // first list line of each bucket in the span
+    // three layout sets, each nb words apart (set k at + k * nb)
+    L.cs = take(3u * nb);    // first valid adjusted position (carried words first)
+    L.ve = take(3u * nb);    // end adjusted position
+    L.ce = take(3u * nb);    // first position of the span's own packets
+    L.sb = take(3u * nb);    // stage index of the bucket's first packet
+    L.rb = take(3u * nb);    // stage index bias: sb - prefix at the span's first chunk
+    L.lsl = take(3u * (nb + 1u));   // first list line of each bucket in the span
     L.misc = take(8);
-    L.tab = take(nb * ((1u << gshift) + 1u));
+    L.tab = take(2u * nb * (1u << gshift));   // raw prefixes, two buffers
     L.cb = take(2u * 16u * nb);     // carried words, two sets
-    L.ltag = take(lmax);            // bucket | copy mode << 30 per line
-    L.stg = take((seg + 2u) / 2u);  // seg 16-bit offsets + the spare
+    L.ltag = take(2u * lmax);       // bucket | flags per line, two buffers
+    L.lsrc = take(2u * lmax);       // stage index of the line's first position (mod 2^32)
+    L.stg_words = (seg + 2u) / 2u;  // seg 16-bit offsets + the spare
+    L.stg = take(2u * L.stg_words);
     L.words = o;
     return L;
 }
 
-// (second bound: waves per SIMD, 4 = two 512-thread workgroups a CU, <= 128 VGPRs)
-__global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
+constexpr int kWideBlock = 2 * kLineBlock;   // placement waves, then copy-out waves
+// (second bound: waves per SIMD, 4 = one 1024-thread workgroup a CU, <= 128 VGPRs)
+__global__ __launch_bounds__(kWideBlock, 4) void yrss_scatter_wide(LineParams P)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
-    const uint32_t nb = P.nb, t = threadIdx.x, lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const uint32_t nb = P.nb, lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    // role: 0 load and place (waves 0-7), 1 copy out (waves 8-15); t is the
+    // thread's index inside its role's 512
+    const bool copier = __builtin_amdgcn_readfirstlane(threadIdx.x / kLineBlock) != 0u;
+    const uint32_t t = threadIdx.x & (kLineBlock - 1u);
     // capacity, before any barrier (uniform): see line_nb_max
     if (nb > kWideNbMax || (nb << P.gshift) > kWideTabMax || P.seg > kWideSpan) {
         if (t == 0)
             report_fault(P.fault, YRSS_FAULT_LINE_CAPACITY, YRSS_K_SCATTER, nb, kWideNbMax);
         return;
     }
+    line_desync(P.desync);
     const WideLds o = wide_lds(nb, P.gshift, P.lmax, P.seg);
-#ifdef YRSS_PROF_LINES
-    if (t == 0 && blockIdx.x < 2048u)
-        g_line_prof[(blockIdx.x * 8u) * 8u + 7u] = __builtin_amdgcn_s_memrealtime();
-#endif
-    uint32_t *start = lsm + o.start, *misc = lsm + o.misc, *tab = lsm + o.tab;
-    uint32_t *const cs_sets = lsm + o.cs, *const ve_sets = lsm + o.ve, *const ce_sets = lsm + o.ce;
-    uint32_t *const sb_sets = lsm + o.sb, *const rb_sets = lsm + o.rb, *const lsl_sets = lsm + o.lsl;
-    uint32_t *const cb_sets = lsm + o.cb, *ltag = lsm + o.ltag;
-    uint16_t *stg = reinterpret_cast<uint16_t *>(lsm + o.stg);
+    uint32_t *start = lsm + o.start, *misc = lsm + o.misc;
     const uint32_t cap = P.seg;   // the spare stage slot
     const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 15u);
     const uint32_t nsp = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
     const uint32_t r = xcd_block(P.xcd), G = gridDim.x;
     const uint32_t g0 = (uint32_t)((uint64_t)r * nsp / G);
     const uint32_t g1 = (uint32_t)((uint64_t)(r + 1u) * nsp / G);
-    const uint32_t ncs = 1u << P.gshift, ntab = nb << P.gshift, rs = ncs + 1u;
+#ifdef YRSS_PROF_LINES
+    if (t == 0 && blockIdx.x < 2048u)
+        g_line_prof[(blockIdx.x * 8u) * 8u + 7u] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const uint32_t ncs = 1u << P.gshift, ntab = nb << P.gshift;
     auto prefix = [&](uint32_t b, uint32_t c) {
         return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : P.totals[b];
     };
@@ -1911,13 +1957,17 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
         const uint64_t e = (uint64_t)g * P.seg + P.seg;
         return e < P.n ? (uint32_t)e : P.n;
     };
+    // per-span buffers: layout set (span g - g0 + 1) mod 3 (set 0 first holds
+    // the state before the range), two-buffer arrays by (g - g0) & 1
+    auto setk = [&](uint32_t g) { return (g - g0 + 1u) % 3u; };
+    auto buf = [&](uint32_t g) { return (g - g0) & 1u; };
     uint32_t pre0 = 0;
     const ListOut lout = list_out(P.qidx, P.n);
-    // the current span's streams and the next span's (issued in (b), waited
-    // for before the copy-out, then moved into the current set: no wait)
-    u32x4 pk[kWideG], qk[kWideG], pkn[kWideG], qkn[kWideG];
-    // wave 0, a bucket to a lane: the prefix at the end of the span it lays
-    // out next (its start is the previous span's end, already in ve)
+    // the span being placed (then the next one's, loaded into the same registers)
+    u32x4 pk[kWideG], qk[kWideG];
+    // the next span's prefixes (all threads, the table) and, for wave 0 a
+    // bucket to a lane, the prefix at that span's end (its start is the
+    // previous span's end, already in ve)
     uint32_t pt[kWideTabRegs], w0e[kWideBI];
     auto load_span = [&](uint32_t g, u32x4 (&lk)[kWideG], u32x4 (&lq)[kWideG]) {
         const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
@@ -1950,7 +2000,7 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
             if (k * kLineBlock < ntab)   // (uniform)
                 pt[k] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)vo, (int)(c0 * 4u + k * step), 0);
     };
-    if (P.early && g0 < g1) {
+    if (P.early && g0 < g1 && !copier) {
         pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
         load_span(g0, pk, qk);
     }
@@ -2008,26 +2058,30 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
     }
     if (g0 >= g1)
         return;
-    if (!P.early) {
+    if (!P.early && !copier) {
         pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
         load_span(g0, pk, qk);
     }
     __builtin_amdgcn_s_waitcnt(kWaitVm0);
-    if (t < nb) {
+    if (!copier && t < nb) {   // set 0: the state before the range's first span
         const uint32_t a = start[t] + pre0 + ph;
-        cs_sets[nb + t] = a;
-        ve_sets[nb + t] = a;
+        lsm[o.cs + t] = a;
+        lsm[o.ve + t] = a;
     }
-    // Wave 0, a bucket to a lane, lays span g out into set s from set s ^ 1
-    // and the prefixes it holds: valid positions [cs, ve) = carried words and
-    // the span's packets, ce the first of the span's own; the list lines (an
-    // exclusive scan over buckets) and the stage index of each bucket's first
-    // packet (an exclusive scan of the span's counts); the table bias rb.
-    auto layout = [&](uint32_t g, uint32_t s) {
-        const uint32_t *pcs = cs_sets + (s ^ 1u) * nb, *pve = ve_sets + (s ^ 1u) * nb;
-        uint32_t *wcs = cs_sets + s * nb, *wve = ve_sets + s * nb, *wce = ce_sets + s * nb;
-        uint32_t *wsb = sb_sets + s * nb, *wrb = rb_sets + s * nb, *wlsl = lsl_sets + s * (nb + 1u);
-        uint32_t lines = 0, pk = 0;
+    // Wave 0, a bucket to a lane, lays span g out into its set from the
+    // previous span's set and w0e: valid positions [cs, ve) = carried words
+    // and the span's packets, ce the first of the span's own; the list lines
+    // (an exclusive scan over buckets), the stage index of each bucket's first
+    // packet (an exclusive scan of the span's counts) and the stage bias rb.
+    // Positions are start + prefix + ph: the span's first is the previous
+    // span's end.
+    auto layout = [&](uint32_t g) {
+        const uint32_t sp = ((g - g0) % 3u) * nb, sw = setk(g) * nb;
+        const uint32_t *pcs = lsm + o.cs + sp, *pve = lsm + o.ve + sp;
+        uint32_t *wcs = lsm + o.cs + sw, *wve = lsm + o.ve + sw, *wce = lsm + o.ce + sw;
+        uint32_t *wsb = lsm + o.sb + sw, *wrb = lsm + o.rb + sw;
+        uint32_t *wlsl = lsm + o.lsl + setk(g) * (nb + 1u);
+        uint32_t lines = 0, pkt = 0;
         const uint32_t ll = opaque(lane);
 #pragma unroll
         for (uint32_t i = 0; i < kWideBI; ++i) {
@@ -2036,8 +2090,6 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
             const uint32_t b = i * kWave + ll;
             uint32_t nl = 0, v0 = 0, e0 = 0, cnt = 0, base = 0;
             if (b < nb) {
-                // positions are start + prefix + ph: the span's first is the
-                // previous span's end, its end the prefix at its end chunk
                 e0 = pve[b];
                 v0 = max(pcs[b], e0 & ~15u);
                 base = start[b] + ph;
@@ -2052,124 +2104,77 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
             const uint32_t y = wave_incl_scan(cnt, lane);
             if (b < nb) {
                 wlsl[b] = lines + x - nl;
-                const uint32_t sbb = pk + y - cnt;
+                const uint32_t sbb = pkt + y - cnt;
                 wsb[b] = sbb;
                 wrb[b] = sbb - (e0 - base);   // sb - prefix at the span's first chunk
             }
             lines += __shfl(x, kWave - 1, kWave);
-            pk += __shfl(y, kWave - 1, kWave);
+            pkt += __shfl(y, kWave - 1, kWave);
         }
         if (lane == 0) {
             const uint32_t len = span_end(g) - g * P.seg;
-            if (lines > P.lmax || pk != len) {
+            if (lines > P.lmax || pkt != len) {
                 report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g, lines);
                 lines = 0;
             }
             wlsl[nb] = lines;
-            misc[4u + s] = lines;
+            misc[4u + setk(g)] = lines;
         }
     };
-    __syncthreads();   // set 1 written
-    if (wave == 0)
-        layout(g0, 0u);
-    __syncthreads();
-    uint32_t wrote = 0, wsum = 0;
-    const uint32_t tk = kLineBlock / nb, tb = t % nb, tj = t / nb;
-    auto span = [&](uint32_t g, uint32_t s) {
-        const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
-        const bool last = g + 1u == g1;
-        const uint32_t *cs = cs_sets + s * nb, *ve = ve_sets + s * nb, *ce = ce_sets + s * nb;
-        const uint32_t *sb = sb_sets + s * nb, *rb = rb_sets + s * nb;
-        const uint32_t *lsl = lsl_sets + s * (nb + 1u);
-        const uint32_t *cbr = cb_sets + s * 16u * nb;           // carried into this span
-        uint32_t *cbw = cb_sets + (s ^ 1u) * 16u * nb;          // carried out of it
-        LPROF(0);
-        // (a) the prefix table with its rows' bias: stage index = tab + rank
+    // span g's raw prefix table, from pt (rows of ncs words)
+    auto write_tab = [&](uint32_t g) {
+        uint32_t *tab = lsm + o.tab + buf(g) * ntab;
 #pragma unroll
         for (uint32_t k = 0; k < kWideTabRegs; ++k) {
             const uint32_t e = k * kLineBlock + t;
             if (k * kLineBlock < ntab && e < ntab)
-                tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k] + rb[e >> P.gshift];
+                tab[e] = pt[k];
         }
-        __syncthreads();
-        LPROF(1);
-        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + s]);
-        // (b) the next span's loads; line tags; every packet's stage offset
-        if (!last)
-            load_span(g + 1u, pkn, qkn);
-        if (tj < tk) {
-            const uint32_t b = opaque(tb);
-            const uint32_t l0 = lsl[b], l1 = L ? min(lsl[b + 1u], L) : 0u, v0 = cs[b], e1 = ve[b];
-            for (uint32_t l = l0 + tj; l < l1; l += tk) {
-                const uint32_t gl = l - l0 + (v0 >> 4);
-                const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
-                                      : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
-                                                                                      : 2u;
-                ltag[l] = b | mode << 30;
-            }
-        }
-        auto place = [&](auto ragged) {
-            uint32_t slot[kWideG][8];
-#pragma unroll
-            for (uint32_t k = 0; k < kWideG; ++k) {
-                const uint32_t o8 = 8u * (k * kLineBlock + t);
-                const uint32_t cc = min(o8 >> P.cshift, ncs - 1u);
-#pragma unroll
-                for (uint32_t j = 0; j < 8u; ++j) {
-                    const uint32_t rk = (pk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu;
-                    const uint32_t b = bucket_of(
-                        (int16_t)((qk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu), P.nq);
-                    slot[k][j] = tab[__umul24(b, rs) + cc] + rk;
-                }
-            }
-#pragma unroll
-            for (uint32_t k = 0; k < kWideG; ++k) {
-                const uint32_t o8 = 8u * (k * kLineBlock + t);
-#pragma unroll
-                for (uint32_t j = 0; j < 8u; ++j)
-                    if (!decltype(ragged)::value || o8 + j < len)
-                        stg[min(slot[k][j], cap)] = (uint16_t)(o8 + j);
-            }
-        };
-        if (len == kWideSpan)
-            place(std::false_type{});
-        else
-            place(std::true_type{});
-        LPROF(2);
-        // the next span's streams and prefixes have arrived (waited before
-        // this span's list stores: vmcnt counts loads and stores in one
-        // queue); wave 0 lays the next span out before the barrier
-        __builtin_amdgcn_s_waitcnt(kWaitVm0);
-        if (!last) {
-#pragma unroll
-            for (uint32_t k = 0; k < kWideG; ++k) {
-                pk[k] = pkn[k];
-                qk[k] = qkn[k];
-            }
-            if (wave == 0)
-                layout(g + 1u, s ^ 1u);
-        }
-        __syncthreads();
-        LPROF(3);
-        // the list word at adjusted position a of bucket b
+    };
+    __syncthreads();   // set 0 written
+    if (wave == 0)
+        layout(g0);
+    if (!copier)
+        write_tab(g0);
+    __syncthreads();
+    uint32_t wrote = 0, wsum = 0;
+    const uint32_t tk = kLineBlock / nb, tb = t % nb, tj = t / nb;
+    // the copy-out of span g (its stage, tags, layout and carried words),
+    // then its unfinished lines carried into the other carry set
+    auto copy_out = [&](uint32_t g) {
+        const uint32_t p0 = g * P.seg;
+        const bool last = g + 1u == g1;
+        const uint32_t sw = setk(g) * nb;
+        const uint32_t *cs = lsm + o.cs + sw, *ve = lsm + o.ve + sw, *ce = lsm + o.ce + sw;
+        const uint32_t *sb = lsm + o.sb + sw, *lsl = lsm + o.lsl + setk(g) * (nb + 1u);
+        const uint32_t *cbr = lsm + o.cb + buf(g) * 16u * nb;
+        uint32_t *cbw = lsm + o.cb + (buf(g) ^ 1u) * 16u * nb;
+        const uint32_t *ltag = lsm + o.ltag + buf(g) * P.lmax, *lsrc = lsm + o.lsrc + buf(g) * P.lmax;
+        const uint16_t *stg = reinterpret_cast<const uint16_t *>(lsm + o.stg + buf(g) * o.stg_words);
+        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + setk(g)]);
         auto word_at = [&](uint32_t b, uint32_t a, uint32_t csb, uint32_t ceb, uint32_t sbb) {
             return a < ceb ? cbr[min(16u * b + (a - csb), 16u * nb - 1u)]
                            : p0 + (uint32_t)stg[min(sbb + (a - ceb), cap)];
         };
-        // (c) copy-out: whole quads of whole and partial lines as 16-byte
-        // stores; carried lines (mode 1) wait for the next span
-        auto copy_quad = [&](uint32_t v, uint32_t tag) {
-            const uint32_t mode = tag >> 30;
-            if (mode == 1u)
+        auto copy_quad = [&](uint32_t v, uint32_t tag, uint32_t src) {
+            if (tag & kTagSkip)
                 return;
-            const uint32_t b = tag & 0xffffu;
-            const uint32_t v0 = cs[b], e1 = ve[b], e0 = ce[b], sbb = sb[b];
-            const uint32_t gl = (v >> 2) - lsl[b] + (v0 >> 4);
-            const uint32_t a0 = 16u * gl + 4u * (v & 3u);
-            if (mode == 2u && !(a0 >= v0 && a0 + 4u <= e1))
-                return;   // a cut quad: the pass below
-            const u32x4 e{word_at(b, a0, v0, e0, sbb), word_at(b, a0 + 1u, v0, e0, sbb),
+            const uint32_t b = tag & 0xffffu, q4 = 4u * (v & 3u);
+            uint32_t a0 = 0;
+            u32x4 e;
+            if (tag & (kTagPartial | kTagCarried)) {
+                const uint32_t v0 = cs[b], e1 = ve[b], e0 = ce[b], sbb = sb[b];
+                a0 = 16u * ((v >> 2) - lsl[b] + (v0 >> 4)) + q4;
+                if (!(a0 >= v0 && a0 + 4u <= e1))
+                    return;   // a cut quad: the pass below
+                e = u32x4{word_at(b, a0, v0, e0, sbb), word_at(b, a0 + 1u, v0, e0, sbb),
                           word_at(b, a0 + 2u, v0, e0, sbb), word_at(b, a0 + 3u, v0, e0, sbb)};
+            } else {
+                a0 = 16u * ((v >> 2) - lsl[b] + (cs[b] >> 4)) + q4;
+                const uint32_t i0 = src + q4;
+                e = u32x4{p0 + (uint32_t)stg[min(i0, cap)], p0 + (uint32_t)stg[min(i0 + 1u, cap)],
+                          p0 + (uint32_t)stg[min(i0 + 2u, cap)], p0 + (uint32_t)stg[min(i0 + 3u, cap)]};
+            }
             const uint32_t d = a0 - ph;
             if (d + 4u <= P.n && d + 4u > d) {
                 list_store4<kListAuxMany>(lout, d, e);
@@ -2181,15 +2186,16 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
         };
         constexpr uint32_t kCopyQ = 2u;
         for (uint32_t v0 = t; v0 < 4u * L; v0 += kCopyQ * kLineBlock) {
-            uint32_t tg[kCopyQ];
+            uint32_t tg[kCopyQ], sr[kCopyQ];
 #pragma unroll
             for (uint32_t i = 0; i < kCopyQ; ++i) {
                 const uint32_t v = v0 + i * kLineBlock;
-                tg[i] = v < 4u * L ? ltag[v >> 2] : 1u << 30;
+                tg[i] = v < 4u * L ? ltag[v >> 2] : kTagSkip;
+                sr[i] = v < 4u * L ? lsrc[v >> 2] : 0u;
             }
 #pragma unroll
             for (uint32_t i = 0; i < kCopyQ; ++i)
-                copy_quad(v0 + i * kLineBlock, tg[i]);
+                copy_quad(v0 + i * kLineBlock, tg[i], sr[i]);
         }
         // the cut quads of partial lines, a thread per (bucket, quad, word)
         for (uint32_t e = t; e < 8u * nb; e += kLineBlock) {
@@ -2212,8 +2218,6 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
                 }
             }
         }
-        LPROF(4);
-        // (d) carry the unfinished last lines into the other set
         if (!last) {
             for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
                 const uint32_t b = e >> 4, j = e & 15u;
@@ -2222,10 +2226,94 @@ __global__ __launch_bounds__(kLineBlock, 4) void yrss_scatter_wide(LineParams P)
                     cbw[e] = word_at(b, nv + j, v0, ce[b], sb[b]);
             }
         }
-        LPROF(5);
     };
-    for (uint32_t g = g0; g < g1; ++g)
-        span(g, (g - g0) & 1u);
+    // the line tags of span g, and every packet of it at its stage index
+    auto place = [&](uint32_t g) {
+        const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
+        const bool last = g + 1u == g1;
+        const uint32_t sw = setk(g) * nb;
+        const uint32_t *cs = lsm + o.cs + sw, *ve = lsm + o.ve + sw, *ce = lsm + o.ce + sw;
+        const uint32_t *sb = lsm + o.sb + sw, *rb = lsm + o.rb + sw;
+        const uint32_t *lsl = lsm + o.lsl + setk(g) * (nb + 1u);
+        uint32_t *ltag = lsm + o.ltag + buf(g) * P.lmax, *lsrc = lsm + o.lsrc + buf(g) * P.lmax;
+        uint16_t *stg = reinterpret_cast<uint16_t *>(lsm + o.stg + buf(g) * o.stg_words);
+        const uint32_t *tab = lsm + o.tab + buf(g) * ntab;
+        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + setk(g)]);
+        if (tj < tk) {
+            const uint32_t b = opaque(tb);
+            const uint32_t l0 = lsl[b], l1 = L ? min(lsl[b + 1u], L) : 0u, v0 = cs[b], e1 = ve[b];
+            const uint32_t e0 = ce[b], src0 = sb[b] - e0;
+            for (uint32_t l = l0 + tj; l < l1; l += tk) {
+                const uint32_t gl = l - l0 + (v0 >> 4), a = 16u * gl;
+                const uint32_t tag = b | (a >= v0 && a + 16u <= e1 ? 0u
+                                          : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u
+                                              ? kTagSkip
+                                              : kTagPartial) |
+                                     (a < e0 ? kTagCarried : 0u);
+                ltag[l] = tag;
+                lsrc[l] = src0 + a;
+            }
+        }
+        // a group at a time: every slot of it read before any stage write
+        // (the thread index hidden from the optimiser: its 32 packet offsets
+        // were hoisted out of the phase loop and spilled)
+        const uint32_t tt = opaque(t);
+#pragma unroll
+        for (uint32_t k0 = 0; k0 < kWideG; k0 += 1u) {
+            uint32_t slot[1][8];
+#pragma unroll
+            for (uint32_t k = k0; k < k0 + 1u; ++k) {
+                const uint32_t o8 = 8u * (k * kLineBlock + tt);
+                const uint32_t cc = min(o8 >> P.cshift, ncs - 1u);
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j) {
+                    const uint32_t rk = (pk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu;
+                    const uint32_t b = bucket_of(
+                        (int16_t)((qk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu), P.nq);
+                    slot[k - k0][j] = tab[(b << P.gshift) + cc] + rb[b] + rk;
+                }
+            }
+#pragma unroll
+            for (uint32_t k = k0; k < k0 + 1u; ++k) {
+                const uint32_t o8 = 8u * (k * kLineBlock + tt);
+#pragma unroll
+                for (uint32_t j = 0; j < 8u; ++j)
+                    if (len == kWideSpan || o8 + j < len)
+                        stg[min(slot[k - k0][j], cap)] = (uint16_t)(o8 + j);
+            }
+        }
+    };
+    // phase c - g0: span c + 1's loads; span c - 1 out; span c placed; wait;
+    // span c + 1 laid out and its table written; the barrier
+    for (uint32_t c = g0; c <= g1; ++c) {
+        const uint32_t g = c;   // (the phase clock's span index)
+        (void)g;
+        LPROF(0);
+        const bool more = c + 1u < g1;
+        if (copier) {
+            if (c > g0)
+                copy_out(c - 1u);
+        } else {
+            // span c placed, then span c + 1's streams loaded into the same
+            // registers (one set: 128 VGPRs at 16 waves a CU); their latency
+            // overlaps the copy-out waves' stores
+            if (c < g1)
+                place(c);
+            if (more)
+                load_span(c + 1u, pk, qk);
+            LPROF(2);
+            __builtin_amdgcn_s_waitcnt(kWaitVm0);
+            LPROF(3);
+            if (more) {
+                if (wave == 0)
+                    layout(c + 1u);
+                write_tab(c + 1u);
+            }
+            LPROF(4);
+        }
+        __syncthreads();
+        LPROF(5);
+    }
     wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
     wsum = __shfl(wave_incl_scan(wsum, lane), kWave - 1, kWave);
     if (lane == 0) {
@@ -3198,6 +3286,8 @@ struct yrss_ctx {
         uint64_t worker_inject = 0;   // ticket whose worker burst fires a list guard
         uint32_t line_groups = 0;     // force the line scatter's kG (2 or 4)
         uint32_t skip_line_check = 0; // launch a line scatter the host check refuses
+        uint32_t line_desync = 0;     // odd line-scatter workgroups start late (100 MHz ticks)
+        uint32_t partial_merge = 0;   // partial list lines as plain stores
     } dbg;
 };
 
@@ -3324,11 +3414,12 @@ LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
 {
     LinePlan p{};
     const uint32_t nb = c->nb, cshift = lay.ct_shift + 6u;
-    // past 128 buckets the wide kernel (two workgroups a CU); the test hook
-    // forces a kernel: 1 wide, 2 / 4 yrss_scatter_lines<kG>
+    // kG = 2 up to 128 buckets, 4 past that; the test hook forces a kernel:
+    // 1 the pipelined yrss_scatter_wide (measured slower),
+    // 2 / 4 yrss_scatter_lines<kG>
     const uint32_t force = c->dbg.line_groups;
-    p.wide = force ? force == 1u : nb > line_nb_max(2);
-    p.groups = p.wide ? kWideG : force ? force : 2u;
+    p.wide = force == 1u;
+    p.groups = p.wide ? kWideG : force ? force : nb > line_nb_max(2) ? 4u : 2u;
     p.fits = (p.wide ? nb <= kWideNbMax : nb <= line_nb_max(p.groups)) &&
              nb <= (uint32_t)kLineBlock;
     const uint32_t smax = p.wide ? kWideSpan : line_span_max(p.groups);
@@ -4225,6 +4316,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         S.xcd = c->tune.scatter_xcd != 0 ? 1u : 0u;
         S.nt = c->nb > kListNtBuckets ? 1u : 0u;
         S.early = c->nb > 16u ? 1u : 0u;
+        S.desync = c->dbg.line_desync;
+        S.merge = c->dbg.partial_merge;
         // persistent: the resident workgroups, each one contiguous range of
         // spans, never more workgroups than spans
         const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
@@ -4232,11 +4325,10 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
             lp.wide ? yrss_scatter_wide
             : lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
                               : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
-        const uint32_t sgrid =
-            std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
+        const uint32_t blk = lp.wide ? (uint32_t)kWideBlock : (uint32_t)kLineBlock;
+        const uint32_t sgrid = std::min(spans, resident_blocks(c, (const void *)fn, blk, lp.lds));
         Timed t(c, YRSS_K_SCATTER);
-        hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(kLineBlock), lp.lds, s, t.a,
-                              t.b, 0, S);
+        hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(blk), lp.lds, s, t.a, t.b, 0, S);
         YRSS_HIP(hipGetLastError());
         return 0;
     }
@@ -5313,6 +5405,22 @@ int yrss_debug_line_groups(yrss_ctx *c, uint32_t groups, int skip_host_check)
         return -EINVAL;
     c->dbg.line_groups = groups;
     c->dbg.skip_line_check = (uint32_t)skip_host_check;
+    return 0;
+}
+
+int yrss_debug_partial_merge(yrss_ctx *c, int on)
+{
+    if (!c || on < 0 || on > 1)
+        return -EINVAL;
+    c->dbg.partial_merge = (uint32_t)on;
+    return 0;
+}
+
+int yrss_debug_line_desync(yrss_ctx *c, uint32_t ticks)
+{
+    if (!c || ticks > 100000u)   // <= 1 ms
+        return -EINVAL;
+    c->dbg.line_desync = ticks;
     return 0;
 }
 #endif
