@@ -86,7 +86,7 @@ def parse_args(argv=None):
                          "configs), reported under configs_extra, never as value ('' = off)")
     ap.add_argument("--test-hooks", default="",
                     help="measurements only: run libyrss_test.so with its yrss_debug_* hooks, "
-                         "k=v[,k=v] (merge, groups, desync); the line says so")
+                         "k=v[,k=v] (merge, groups); the line says so")
     ap.add_argument("--dry", action="store_true",
                     help="plumbing check without a GPU (rank spawn, barrier, reductions); "
                          "prints a line marked dry, never a measurement")
@@ -823,8 +823,6 @@ def main(argv=None):
         abi.check(eng._lib.yrss_debug_partial_merge(eng._ctx, hooks["merge"]), "partial_merge")
     if "groups" in hooks:
         abi.check(eng._lib.yrss_debug_line_groups(eng._ctx, hooks["groups"], 0), "line_groups")
-    if "desync" in hooks:
-        abi.check(eng._lib.yrss_debug_line_desync(eng._ctx, hooks["desync"]), "line_desync")
     if args.tune:
         eng.set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in args.tune.split(","))})
     n = args.pkts

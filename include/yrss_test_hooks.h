@@ -22,18 +22,13 @@ extern "C" {
  * per-burst fault path of yrss_worker_poll.  0 disables. */
 int yrss_debug_worker_inject(yrss_ctx *ctx, uint64_t ticket);
 
-/* Force the line scatter's kernel: 1 yrss_scatter_wide, 2 or 4
- * yrss_scatter_lines<kG> (8-packet groups a thread), 0 = the built-in choice
- * (wide past 128 buckets, else kG = 2).  A pairing whose per-bucket arrays cannot
+/* Force the line scatter's instantiation: 2 or 4 yrss_scatter_lines<kG>
+ * (8-packet groups a thread), 0 = the built-in choice (kG = 2 up to 128
+ * buckets, 4 past that).  A pairing whose per-bucket arrays cannot
  * hold nb_queues + 1 buckets makes yrss_dispatch_dev return -EINVAL before
  * anything is launched; with skip_host_check = 1 it is launched anyway, and
  * the kernel's entry check must report YRSS_FAULT_LINE_CAPACITY and leave. */
 int yrss_debug_line_groups(yrss_ctx *ctx, uint32_t groups, int skip_host_check);
-
-/* Odd line-scatter workgroups wait this many 100 MHz ticks (<= 100000)
- * before starting: a measurement of what the workgroups' lockstep costs
- * (results unchanged).  0 disables. */
-int yrss_debug_line_desync(yrss_ctx *ctx, uint32_t ticks);
 
 /* 1: the partial list lines of a workgroup's range (its first and last line
  * of each bucket, the other part written by the neighbouring range) leave as

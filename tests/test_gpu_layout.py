@@ -223,28 +223,39 @@ def test_line_scatter_capacity_is_enforced(dev, oracle_mod):
 @pytest.mark.parametrize("n", [8191, 8193, 300001, (1 << 22) + 77])
 @pytest.mark.parametrize("cfg", [(128, 128, 1, 0), (200, 200, 1, 1), (256, 256, 1, 0),
                                  (4096, 256, 1, 1)])
-def test_wide_scatter_bucket_counts(dev, oracle_mod, cfg, n):
-    """Past 128 buckets the lists come from yrss_scatter_wide (8192-packet
-    spans, 16-bit compact stage, two carry sets): 129 to 257 buckets, spans
-    cut short by n, fuzz and IMIX, filter on and off, compared in full."""
+def test_many_bucket_counts(dev, oracle_mod, cfg, n):
+    """129 to 257 buckets (the kG = 4 line scatter, rank beside q), spans cut
+    short by n, fuzz, TCP and IMIX, filter on and off, compared in full."""
     with SoftRss(*cfg, device=0, max_burst=0) as eng:
         for profile, filt in ((abi.SYN_FUZZ, False), (abi.SYN_IMIX, True), (abi.SYN_TCP4, False)):
             check(eng, oracle_mod, cfg, profile, n, first=n + 7, want_filter=filt)
 
 
-@pytest.mark.parametrize("groups", [1, 4])
-@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (64, 64, 1, 0), (255, 255, 1, 0)])
+@pytest.mark.parametrize("groups", [2, 4])
+@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (64, 64, 1, 0), (127, 127, 1, 0)])
 def test_forced_line_kernels(dev, oracle_mod, cfg, groups):
-    """Every line-scatter kernel gives the same lists wherever it is allowed
-    to run: the wide kernel forced below 128 buckets (1), the 16 384-packet
-    kG = 4 kernel (4), through libyrss_test.so's hook; chunk and span
-    overrides on top."""
+    """Both line-scatter instantiations give the same lists wherever they
+    may run: the 16 384-packet kG = 4 kernel forced below 128 buckets, through
+    libyrss_test.so's hook; chunk and span overrides on top."""
     with SoftRss(*cfg, device=0, max_burst=0, lib_path=str(abi.TEST_LIB_PATH)) as eng:
         assert eng._lib.yrss_debug_line_groups(eng._ctx, groups, 0) == 0
         for profile in (abi.SYN_TCP4, abi.SYN_FUZZ):
             check(eng, oracle_mod, cfg, profile, 777777, first=41)
         eng.set_tuning(chunk_tiles=16, span_tiles=64)
         check(eng, oracle_mod, cfg, abi.SYN_FUZZ, 1 << 20, first=3)
+
+
+@pytest.mark.parametrize("cfg", [(8, 8, 1, 0), (64, 64, 1, 1), (255, 255, 1, 0)])
+def test_partial_line_merge_parity(dev, oracle_mod, cfg):
+    """The partial list lines of each workgroup's range written with plain
+    stores (yrss_debug_partial_merge: the two parts meet in L2) give the same
+    lists, XCD mapping on and off (off: neighbouring ranges on other XCDs)."""
+    with SoftRss(*cfg, device=0, max_burst=0, lib_path=str(abi.TEST_LIB_PATH)) as eng:
+        assert eng._lib.yrss_debug_partial_merge(eng._ctx, 1) == 0
+        for xcd in (1, 0):
+            eng.set_tuning(scatter_xcd=xcd)
+            for profile in (abi.SYN_TCP4, abi.SYN_FUZZ):
+                check(eng, oracle_mod, cfg, profile, (1 << 22) + 999, first=7)
 
 
 def test_tuning_rejects_bad_values(dev):

@@ -51,7 +51,7 @@ def main() -> int:
         path, _, tune = s.partition("@")
         tune = tune or args.tune
         # "test": libyrss_test.so, whose hooks the dbg_* keys drive
-        # (dbg_groups: yrss_debug_line_groups, dbg_desync: yrss_debug_line_desync)
+        # (dbg_groups: yrss_debug_line_groups, dbg_merge: yrss_debug_partial_merge)
         lib = None if path == "cur" else str(abi.TEST_LIB_PATH) if path == "test" \
             else str(ROOT / path)
         specs.append((s, lib,
@@ -74,13 +74,11 @@ def main() -> int:
                 tn = dict(tune)
                 # side=1: the caller's work on a non-default (non-blocking) stream
                 st = torch.cuda.Stream() if tn.pop("side", 0) else None
-                grp, des = tn.pop("dbg_groups", 0), tn.pop("dbg_desync", 0)
+                grp = tn.pop("dbg_groups", 0)
                 if tn.pop("dbg_merge", 0):
                     assert e._lib.yrss_debug_partial_merge(e._ctx, 1) == 0
                 if grp:
                     assert e._lib.yrss_debug_line_groups(e._ctx, grp, 0) == 0
-                if des:
-                    assert e._lib.yrss_debug_line_desync(e._ctx, des) == 0
                 if tn:
                     e.set_tuning(**tn)
                 wins = [e.synth(PROFILES[args.profile], n, k * n, stride=stride)

@@ -38,7 +38,7 @@ check)
     ;;
 wide1)
     step tests_wide 400 python -u -m pytest tests/test_gpu_layout.py -x -q --timeout 120 \
-        --timeout-method thread -k "wide or forced_line or capacity or bucket_counts" || exit 1
+        --timeout-method thread -k "many_bucket or forced_line or capacity or bucket_counts" || exit 1
     step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit 1
     step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-3,64,129,255}" \
         --libs "cur,ablib/libyrss_r05base.so" --rounds "${AB_ROUNDS:-6}" || exit 1
@@ -58,7 +58,7 @@ wide1)
     ;;
 wide2)
     step tests_wide 400 python -u -m pytest tests/test_gpu_layout.py -x -q --timeout 120 \
-        --timeout-method thread -k "wide or forced_line or capacity or bucket_counts or xcd" || exit 1
+        --timeout-method thread -k "many_bucket or forced_line or capacity or bucket_counts or xcd" || exit 1
     step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-129,255}" \
         --libs "test,test@dbg_groups=1" --rounds "${AB_ROUNDS:-4}" || exit 1
     tools/build_ab_lib.sh prof -DYRSS_PROF_LINES=1 -DYRSS_TEST_HOOKS=1 > gpurun_out/build_prof.log 2>&1 || exit 1
@@ -87,12 +87,13 @@ skel)
         done
     done
     ;;
-desync)
-    L="test@dbg_groups=4,test@dbg_groups=4;dbg_desync=250,test@dbg_groups=4;dbg_desync=500"
-    L="$L,test@dbg_groups=1,test@dbg_groups=1;dbg_desync=300"
-    step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-255,129}" --libs "$L" \
-        --rounds "${AB_ROUNDS:-4}" || exit 1
-    cat gpurun_out/ab.log
+merge)
+    step tests 400 python -u -m pytest tests/test_gpu_layout.py tests/test_gpu_worker.py -x -q \
+        --timeout 120 --timeout-method thread -k "many_bucket or forced_line or capacity or merge or guard" || exit 1
+    step ab 1200 python tools/ab_inproc.py --nb-procs "${AB_Q:-8,64,255}" \
+        --libs "test,test@dbg_merge=1" --rounds "${AB_ROUNDS:-8}" || exit 1
+    step winab 600 python tools/win_ab.py --pools 1048576,16384 || exit 1
+    cat gpurun_out/ab.log gpurun_out/winab.log
     ;;
 prof)
     # the line scatter's phase clock (a tools build with the test hooks)

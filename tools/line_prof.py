@@ -24,8 +24,6 @@ import torch  # noqa: E402
 from yastack_amd import SoftRss, abi  # noqa: E402
 
 PH = ["a tab + layout + S1", "b tags/carried/place", "wait + S2", "c copy-out", "d carry"]
-# yrss_scatter_wide (the pipelined kernel past 128 buckets): stamps per phase
-PH_PIPE = ["loads + copy-out c-1", "tags + place c", "wait", "layout + tab c+1", "barrier"]
 
 
 def main() -> int:
@@ -34,14 +32,9 @@ def main() -> int:
     ap.add_argument("--nb-procs", default="8,64")
     ap.add_argument("--pkts", type=int, default=1 << 24)
     ap.add_argument("--groups", type=int, default=0,
-                    help="force the line-scatter kernel (yrss_debug_line_groups: 1 wide, 2 / 4 "
-                         "kG); needs a -DYRSS_TEST_HOOKS build")
-    ap.add_argument("--pipe", action="store_true",
-                    help="phase names of the pipelined wide kernel (past 128 buckets)")
+                    help="force the line-scatter kernel (yrss_debug_line_groups: 2 / 4 kG); "
+                         "needs a -DYRSS_TEST_HOOKS build")
     args = ap.parse_args()
-    global PH
-    if args.pipe:
-        PH = PH_PIPE
     lib = abi.load(str(ROOT / args.lib))
     lib.yrss_debug_line_prof.restype = ctypes.c_int
     lib.yrss_debug_line_prof.argtypes = [ctypes.c_void_p, ctypes.c_size_t]

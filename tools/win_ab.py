@@ -25,11 +25,15 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--bursts", default="32,1024")
+    ap.add_argument("--pools", default=str(1 << 20),
+                    help="mbuf pool sizes: 2^20 is cache-cold (2.4 GB); 16384 keeps the touched "
+                         "header and window lines LLC-resident, as an rx ring's recycled mbufs")
     args = ap.parse_args()
     place = bench.gpu_placement(bench.device_identity(0, False))
     print(json.dumps({"placement": place}), flush=True)
     exe = ROOT / "tools" / "yrss_cbench"
-    for burst in (int(b) for b in args.bursts.split(",")):
+    for pool, burst in ((int(p), int(b)) for p in args.pools.split(",")
+                        for b in args.bursts.split(",")):
         blocks = 128 if burst <= 64 else 32
         for r in range(args.rounds):
             for nt in ("0", "1"):
@@ -40,14 +44,14 @@ def main() -> int:
                        "YRSS_CBENCH_WIN_NT": nt}
                 if place.get("dispatch_cpu") is not None:
                     env["YRSS_CBENCH_CPU"] = str(place["dispatch_cpu"])
-                out = subprocess.run([str(exe), "1", str(1 << 20), str(burst), "1"],
+                out = subprocess.run([str(exe), "1", str(pool), str(burst), "1"],
                                      capture_output=True, text=True, timeout=240, env=env)
                 for line in out.stdout.splitlines():
                     try:
                         d = json.loads(line)
                     except ValueError:
                         continue
-                    print(json.dumps({"burst": burst, "round": r, "win_nt": int(nt),
+                    print(json.dumps({"pool": pool, "burst": burst, "round": r, "win_nt": int(nt),
                                       "mpps": d["mpps"], "submit_cycles": d.get("submit_cycles"),
                                       "poll_cycles": d.get("poll_cycles"), "cpu": d.get("cpu")}),
                           flush=True)

@@ -240,7 +240,6 @@ _PROTOS = {
 _TEST_PROTOS = {
     "yrss_debug_worker_inject": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "yrss_debug_line_groups": (ctypes.c_int, [_vp, _u32, ctypes.c_int]),
-    "yrss_debug_line_desync": (ctypes.c_int, [_vp, _u32]),
     "yrss_debug_partial_merge": (ctypes.c_int, [_vp, ctypes.c_int]),
 }
 

@@ -1243,7 +1243,6 @@ struct LineParams {
     uint32_t xcd;              // workgroups of one XCD take consecutive ranges
     uint32_t nt;               // list stores non-temporal only (no sc1): past 64 buckets
     uint32_t early;            // first span's loads before the totals: past 16 buckets
-    uint32_t desync;           // test builds only: odd workgroups start this many 100 MHz ticks late
     uint32_t merge;            // partial lines (a range's first / last) as plain stores: L2 merges
 };
 
@@ -1328,22 +1327,6 @@ __device__ uint64_t g_line_prof[2048 * 8 * 8];
     } while (0)
 #endif
 
-// Test builds only (yrss_debug_line_desync): odd workgroups start late, so
-// that neighbouring workgroups' read and write phases interleave instead of
-// running in lockstep (a measurement of the lockstep's cost)
-__device__ __forceinline__ void line_desync(uint32_t ticks)
-{
-#ifdef YRSS_TEST_HOOKS
-    if (ticks && (blockIdx.x & 1u)) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < ticks)
-            __builtin_amdgcn_s_sleep(8);
-    }
-#else
-    (void)ticks;
-#endif
-}
-
 template <bool kPacked, uint32_t kG>
 __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lines(LineParams P)
 {
@@ -1358,7 +1341,6 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             report_fault(P.fault, YRSS_FAULT_LINE_CAPACITY, YRSS_K_SCATTER, nb, line_nb_max(kG));
         return;
     }
-    line_desync(P.desync);
     const LineLds o = line_lds(nb, P.gshift, P.lmax);
 #ifdef YRSS_PROF_LINES
     if (t == 0 && blockIdx.x < 2048u)   // kernel entry, slot 7 of span 0
@@ -1818,502 +1800,6 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             span(g + 1u, 1u, pkB, qkB, pkA, qkA);
     }
     // every packet of the range left exactly once
-    wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
-    wsum = __shfl(wave_incl_scan(wsum, lane), kWave - 1, kWave);
-    if (lane == 0) {
-        atomicAdd(&misc[3], wrote);
-        atomicAdd(&misc[1], wsum);
-    }
-    __syncthreads();
-    if (t == 0) {
-        const uint64_t a = (uint64_t)g0 * P.seg, e = span_end(g1 - 1u);
-        const uint32_t want = (uint32_t)(e - a);
-        const uint32_t want_sum = (uint32_t)((e - a) * (a + e - 1u) / 2u);
-        if (misc[3] != want)
-            report_fault(P.fault, YRSS_FAULT_COUNT_MISMATCH, YRSS_K_SCATTER, g0, misc[3]);
-        else if (misc[1] != want_sum)
-            report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g0, misc[1]);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Kernel 3 (ranked, many buckets): the lists in whole lines, software-
-// pipelined (round 5).
-//
-// Past 128 buckets yrss_scatter_lines runs 16 384-packet spans at one
-// workgroup per CU (145 KB of LDS), and its phase clock at 256 buckets shows
-// what a span costs (profiles/r05_lineprof_wide1.log): every workgroup runs
-// the same schedule, so the chip reads the next span's streams in one phase
-// (placement + wait, 4.4 us) and writes the lists in another (copy-out,
-// 5.5 us), with LDS-only phases (tags, carry, layout) between them, while the
-// list writes alone take 13-15 us for 2^24 packets at any bucket count
-// (tools/list_write_bw.hip, profiles/r05_list_write_bw.log).  Two workgroups
-// a CU in 80 KB (8192-packet spans) did not help: they run in the same
-// lockstep (r05 A/B: scatter 57.6 against 53.0 us at 256 buckets).
-//
-// Here a 1024-thread workgroup splits its waves: in one phase waves 0-7
-// issue span c + 1's loads, tag and place span c into one stage, wait for the
-// loads, lay span c + 1 out and write its prefix table, while waves 8-15 copy
-// span c - 1 out of the other stage and carry its unfinished lines; both meet
-// at the phase's only barrier.  A wave stalled on its stores (the chip's list
-// writes) no longer holds up the placement behind it in program order, and
-// the copy-out waves' stores do not sit in the placement waves' vmcnt queue.
-// (One 512-thread group doing both in turn, the first form of this kernel,
-// was slower: its stores stalled it before it could place.)  So the
-// stage, the line tags and the prefix table come in two buffers, the
-// per-bucket layout in three sets (span c - 1's copy-out, span c's tags and
-// placement, span c + 1's layout), the carried words in two.
-// - The stage is compact and 16-bit: a span's packets sorted by bucket as
-//   offsets from the span's first packet (no line padding); a packet's stage
-//   index is tab[b][chunk] + rb[b] + rank with tab the raw prefixes.
-// - The words carried from earlier spans (a bucket's unfinished last line,
-//   <= 15) stay 32-bit: a list word at adjusted position a of bucket b is
-//   cb[b][a - cs[b]] below ce[b], else p0 + stage[sb[b] + a - ce[b]].
-// - Each list line is tagged with its bucket, flags and the stage index of
-//   its first position, so a whole line's quad is two LDS reads and four
-//   stage halfwords.
-// Same outputs, checks and fault records as yrss_scatter_lines; it always
-// reads the rank beside q (the bucket does not pack beside it at these
-// chunks).
-// ---------------------------------------------------------------------------
-constexpr uint32_t kWideG = 4;                             // 8-packet groups a thread
-constexpr uint32_t kWideSpan = kLineBlock * 8u * kWideG;   // 16384 packets
-constexpr uint32_t kWideBI = 5;                            // buckets a wave-0 lane holds
-constexpr uint32_t kWideNbMax = 64u * kWideBI;             // 320 (nb <= 257 in use)
-constexpr uint32_t kWideTabRegs = 5;                       // nb x span chunks <= 2560
-constexpr uint32_t kWideTabMax = kLineBlock * kWideTabRegs;
-// line tag: bucket in the low 16 bits and
-constexpr uint32_t kTagSkip = 1u << 31;      // carried to the next span, not stored now
-constexpr uint32_t kTagPartial = 1u << 30;   // a range's first / last line: cut quads by the pass
-constexpr uint32_t kTagCarried = 1u << 29;   // holds carried words: read through word_at
-
-struct WideLds {
-    uint32_t start, cs, ve, ce, sb, rb, lsl, misc, tab, cb, ltag, lsrc, stg, stg_words, words;
-};
-__host__ __device__ inline WideLds wide_lds(uint32_t nb, uint32_t gshift, uint32_t lmax,
-                                            uint32_t seg)
-{
-    WideLds L;
-    uint32_t o = 0;
-    auto take = [&](uint32_t w) {
-        const uint32_t at = o;
-        o = (o + w + 3u) & ~3u;
-        return at;
-    };
-    L.start = take(nb);
-    // three layout sets, each nb words apart (set k at + k * nb)
-    L.cs = take(3u * nb);    // first valid adjusted position (carried words first)
-    L.ve = take(3u * nb);    // end adjusted position
-    L.ce = take(3u * nb);    // first position of the span's own packets
-    L.sb = take(3u * nb);    // stage index of the bucket's first packet
-    L.rb = take(3u * nb);    // stage index bias: sb - prefix at the span's first chunk
-    L.lsl = take(3u * (nb + 1u));   // first list line of each bucket in the span
-    L.misc = take(8);
-    L.tab = take(2u * nb * (1u << gshift));   // raw prefixes, two buffers
-    L.cb = take(2u * 16u * nb);     // carried words, two sets
-    L.ltag = take(2u * lmax);       // bucket | flags per line, two buffers
-    L.lsrc = take(2u * lmax);       // stage index of the line's first position (mod 2^32)
-    L.stg_words = (seg + 2u) / 2u;  // seg 16-bit offsets + the spare
-    L.stg = take(2u * L.stg_words);
-    L.words = o;
-    return L;
-}
-
-constexpr int kWideBlock = 2 * kLineBlock;   // placement waves, then copy-out waves
-// (second bound: waves per SIMD, 4 = one 1024-thread workgroup a CU, <= 128 VGPRs)
-__global__ __launch_bounds__(kWideBlock, 4) void yrss_scatter_wide(LineParams P)
-{
-    extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
-    const uint32_t nb = P.nb, lane = lane_id();
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-    // role: 0 load and place (waves 0-7), 1 copy out (waves 8-15); t is the
-    // thread's index inside its role's 512
-    const bool copier = __builtin_amdgcn_readfirstlane(threadIdx.x / kLineBlock) != 0u;
-    const uint32_t t = threadIdx.x & (kLineBlock - 1u);
-    // capacity, before any barrier (uniform): see line_nb_max
-    if (nb > kWideNbMax || (nb << P.gshift) > kWideTabMax || P.seg > kWideSpan) {
-        if (t == 0)
-            report_fault(P.fault, YRSS_FAULT_LINE_CAPACITY, YRSS_K_SCATTER, nb, kWideNbMax);
-        return;
-    }
-    line_desync(P.desync);
-    const WideLds o = wide_lds(nb, P.gshift, P.lmax, P.seg);
-    uint32_t *start = lsm + o.start, *misc = lsm + o.misc;
-    const uint32_t cap = P.seg;   // the spare stage slot
-    const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 15u);
-    const uint32_t nsp = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
-    const uint32_t r = xcd_block(P.xcd), G = gridDim.x;
-    const uint32_t g0 = (uint32_t)((uint64_t)r * nsp / G);
-    const uint32_t g1 = (uint32_t)((uint64_t)(r + 1u) * nsp / G);
-#ifdef YRSS_PROF_LINES
-    if (t == 0 && blockIdx.x < 2048u)
-        g_line_prof[(blockIdx.x * 8u) * 8u + 7u] = __builtin_amdgcn_s_memrealtime();
-#endif
-    const uint32_t ncs = 1u << P.gshift, ntab = nb << P.gshift;
-    auto prefix = [&](uint32_t b, uint32_t c) {
-        return c < P.nchunk ? P.seg_off[(size_t)b * P.ncol + c] : P.totals[b];
-    };
-    auto span_end = [&](uint32_t g) {
-        const uint64_t e = (uint64_t)g * P.seg + P.seg;
-        return e < P.n ? (uint32_t)e : P.n;
-    };
-    // per-span buffers: layout set (span g - g0 + 1) mod 3 (set 0 first holds
-    // the state before the range), two-buffer arrays by (g - g0) & 1
-    auto setk = [&](uint32_t g) { return (g - g0 + 1u) % 3u; };
-    auto buf = [&](uint32_t g) { return (g - g0) & 1u; };
-    uint32_t pre0 = 0;
-    const ListOut lout = list_out(P.qidx, P.n);
-    // the span being placed (then the next one's, loaded into the same registers)
-    u32x4 pk[kWideG], qk[kWideG];
-    // the next span's prefixes (all threads, the table) and, for wave 0 a
-    // bucket to a lane, the prefix at that span's end (its start is the
-    // previous span's end, already in ve)
-    uint32_t pt[kWideTabRegs], w0e[kWideBI];
-    auto load_span = [&](uint32_t g, u32x4 (&lk)[kWideG], u32x4 (&lq)[kWideG]) {
-        const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
-        load_groups(P.rank, p0, pe, tt, lk);
-        load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, lq);
-        const uint32_t c0 = g << P.gshift;
-        if (wave == 0) {
-            const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
-            const __amdgpu_buffer_rsrc_t rtot = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint32_t *>(P.totals), 0, (int)(nb * 4u), kRsrcWord3);
-            const bool inner = c0 + ncs < P.nchunk;
-            const uint32_t ll = opaque(lane);
-#pragma unroll
-            for (uint32_t i = 0; i < kWideBI; ++i) {
-                if (i * kWave < nb) {   // (uniform)
-                    const uint32_t b = i * kWave + ll;
-                    w0e[i] = inner ? __builtin_amdgcn_raw_buffer_load_b32(
-                                         rs0, (int)(b * P.ncol * 4u), (int)((c0 + ncs) * 4u), 0)
-                                   : __builtin_amdgcn_raw_buffer_load_b32(rtot, (int)(b * 4u), 0, 0);
-                }
-            }
-        }
-        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t *>(P.seg_off), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
-        const uint32_t vo = ((tt >> P.gshift) * P.ncol + (tt & (ncs - 1u))) * 4u;
-        const uint32_t step = (kLineBlock >> P.gshift) * P.ncol * 4u;
-#pragma unroll
-        for (uint32_t k = 0; k < kWideTabRegs; ++k)
-            if (k * kLineBlock < ntab)   // (uniform)
-                pt[k] = __builtin_amdgcn_raw_buffer_load_b32(rr, (int)vo, (int)(c0 * 4u + k * step), 0);
-    };
-    if (P.early && g0 < g1 && !copier) {
-        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
-        load_span(g0, pk, qk);
-    }
-    // list starts (exclusive scan of totals), every block's total loaded at once
-    if (wave == 0) {
-        uint32_t tv[kWideBI];
-#pragma unroll
-        for (uint32_t i = 0; i < kWideBI; ++i) {
-            const uint32_t b = i * kWave + lane;
-            tv[i] = i * kWave < nb && b < nb ? P.totals[b] : 0u;
-        }
-        uint32_t carry = 0, nzb = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < kWideBI; ++i) {
-            if (i * kWave >= nb)   // (uniform)
-                break;
-            const uint32_t b = i * kWave + lane;
-            const uint32_t x0 = tv[i];
-            nzb += (uint32_t)__popcll(__ballot(x0 != 0u));
-            const uint32_t x = wave_incl_scan(x0, lane);
-            if (b < nb) {
-                start[b] = carry + x - x0;
-                if (blockIdx.x == 0)
-                    P.qstart[b] = carry + x - x0;
-            }
-            carry += __shfl(x, kWave - 1, kWave);
-        }
-        if (lane == 0) {
-            if (blockIdx.x == 0)
-                P.qstart[nb] = carry;
-            misc[0] = nzb;
-            misc[1] = 0u;
-            misc[3] = 0u;
-        }
-    }
-    __syncthreads();
-    if (misc[0] == 1u) {
-        // one non-empty list: 0, 1, ..., n-1 (as yrss_scatter_lines)
-        const ListOut lo = list_out(P.qidx, P.n);
-        const uint32_t ph4 = ph & 3u;
-        const uint32_t head = min(P.n, (4u - ph4) & 3u);
-        const uint32_t nv = (P.n - head) >> 2;
-        const uint32_t T = gridDim.x * blockDim.x;
-        const uint32_t id = blockIdx.x * blockDim.x + t;
-        if (id < head)
-            list_store1<kListAux>(lo, id, id);
-        for (uint32_t v = id; v < nv; v += T) {
-            const uint32_t x = head + 4u * v;
-            list_store4<kListAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
-        }
-        const uint32_t e = head + 4u * nv + id;
-        if (e < P.n)
-            list_store1<kListAux>(lo, e, e);
-        return;
-    }
-    if (g0 >= g1)
-        return;
-    if (!P.early && !copier) {
-        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
-        load_span(g0, pk, qk);
-    }
-    __builtin_amdgcn_s_waitcnt(kWaitVm0);
-    if (!copier && t < nb) {   // set 0: the state before the range's first span
-        const uint32_t a = start[t] + pre0 + ph;
-        lsm[o.cs + t] = a;
-        lsm[o.ve + t] = a;
-    }
-    // Wave 0, a bucket to a lane, lays span g out into its set from the
-    // previous span's set and w0e: valid positions [cs, ve) = carried words
-    // and the span's packets, ce the first of the span's own; the list lines
-    // (an exclusive scan over buckets), the stage index of each bucket's first
-    // packet (an exclusive scan of the span's counts) and the stage bias rb.
-    // Positions are start + prefix + ph: the span's first is the previous
-    // span's end.
-    auto layout = [&](uint32_t g) {
-        const uint32_t sp = ((g - g0) % 3u) * nb, sw = setk(g) * nb;
-        const uint32_t *pcs = lsm + o.cs + sp, *pve = lsm + o.ve + sp;
-        uint32_t *wcs = lsm + o.cs + sw, *wve = lsm + o.ve + sw, *wce = lsm + o.ce + sw;
-        uint32_t *wsb = lsm + o.sb + sw, *wrb = lsm + o.rb + sw;
-        uint32_t *wlsl = lsm + o.lsl + setk(g) * (nb + 1u);
-        uint32_t lines = 0, pkt = 0;
-        const uint32_t ll = opaque(lane);
-#pragma unroll
-        for (uint32_t i = 0; i < kWideBI; ++i) {
-            if (i * kWave >= nb)   // (uniform)
-                break;
-            const uint32_t b = i * kWave + ll;
-            uint32_t nl = 0, v0 = 0, e0 = 0, cnt = 0, base = 0;
-            if (b < nb) {
-                e0 = pve[b];
-                v0 = max(pcs[b], e0 & ~15u);
-                base = start[b] + ph;
-                const uint32_t e1 = base + w0e[i];
-                cnt = e1 - e0;
-                wcs[b] = v0;
-                wce[b] = e0;
-                wve[b] = e1;
-                nl = ((e1 + 15u) >> 4) - (v0 >> 4);
-            }
-            const uint32_t x = wave_incl_scan(nl, lane);
-            const uint32_t y = wave_incl_scan(cnt, lane);
-            if (b < nb) {
-                wlsl[b] = lines + x - nl;
-                const uint32_t sbb = pkt + y - cnt;
-                wsb[b] = sbb;
-                wrb[b] = sbb - (e0 - base);   // sb - prefix at the span's first chunk
-            }
-            lines += __shfl(x, kWave - 1, kWave);
-            pkt += __shfl(y, kWave - 1, kWave);
-        }
-        if (lane == 0) {
-            const uint32_t len = span_end(g) - g * P.seg;
-            if (lines > P.lmax || pkt != len) {
-                report_fault(P.fault, YRSS_FAULT_STAGE, YRSS_K_SCATTER, g, lines);
-                lines = 0;
-            }
-            wlsl[nb] = lines;
-            misc[4u + setk(g)] = lines;
-        }
-    };
-    // span g's raw prefix table, from pt (rows of ncs words)
-    auto write_tab = [&](uint32_t g) {
-        uint32_t *tab = lsm + o.tab + buf(g) * ntab;
-#pragma unroll
-        for (uint32_t k = 0; k < kWideTabRegs; ++k) {
-            const uint32_t e = k * kLineBlock + t;
-            if (k * kLineBlock < ntab && e < ntab)
-                tab[e] = pt[k];
-        }
-    };
-    __syncthreads();   // set 0 written
-    if (wave == 0)
-        layout(g0);
-    if (!copier)
-        write_tab(g0);
-    __syncthreads();
-    uint32_t wrote = 0, wsum = 0;
-    const uint32_t tk = kLineBlock / nb, tb = t % nb, tj = t / nb;
-    // the copy-out of span g (its stage, tags, layout and carried words),
-    // then its unfinished lines carried into the other carry set
-    auto copy_out = [&](uint32_t g) {
-        const uint32_t p0 = g * P.seg;
-        const bool last = g + 1u == g1;
-        const uint32_t sw = setk(g) * nb;
-        const uint32_t *cs = lsm + o.cs + sw, *ve = lsm + o.ve + sw, *ce = lsm + o.ce + sw;
-        const uint32_t *sb = lsm + o.sb + sw, *lsl = lsm + o.lsl + setk(g) * (nb + 1u);
-        const uint32_t *cbr = lsm + o.cb + buf(g) * 16u * nb;
-        uint32_t *cbw = lsm + o.cb + (buf(g) ^ 1u) * 16u * nb;
-        const uint32_t *ltag = lsm + o.ltag + buf(g) * P.lmax, *lsrc = lsm + o.lsrc + buf(g) * P.lmax;
-        const uint16_t *stg = reinterpret_cast<const uint16_t *>(lsm + o.stg + buf(g) * o.stg_words);
-        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + setk(g)]);
-        auto word_at = [&](uint32_t b, uint32_t a, uint32_t csb, uint32_t ceb, uint32_t sbb) {
-            return a < ceb ? cbr[min(16u * b + (a - csb), 16u * nb - 1u)]
-                           : p0 + (uint32_t)stg[min(sbb + (a - ceb), cap)];
-        };
-        auto copy_quad = [&](uint32_t v, uint32_t tag, uint32_t src) {
-            if (tag & kTagSkip)
-                return;
-            const uint32_t b = tag & 0xffffu, q4 = 4u * (v & 3u);
-            uint32_t a0 = 0;
-            u32x4 e;
-            if (tag & (kTagPartial | kTagCarried)) {
-                const uint32_t v0 = cs[b], e1 = ve[b], e0 = ce[b], sbb = sb[b];
-                a0 = 16u * ((v >> 2) - lsl[b] + (v0 >> 4)) + q4;
-                if (!(a0 >= v0 && a0 + 4u <= e1))
-                    return;   // a cut quad: the pass below
-                e = u32x4{word_at(b, a0, v0, e0, sbb), word_at(b, a0 + 1u, v0, e0, sbb),
-                          word_at(b, a0 + 2u, v0, e0, sbb), word_at(b, a0 + 3u, v0, e0, sbb)};
-            } else {
-                a0 = 16u * ((v >> 2) - lsl[b] + (cs[b] >> 4)) + q4;
-                const uint32_t i0 = src + q4;
-                e = u32x4{p0 + (uint32_t)stg[min(i0, cap)], p0 + (uint32_t)stg[min(i0 + 1u, cap)],
-                          p0 + (uint32_t)stg[min(i0 + 2u, cap)], p0 + (uint32_t)stg[min(i0 + 3u, cap)]};
-            }
-            const uint32_t d = a0 - ph;
-            if (d + 4u <= P.n && d + 4u > d) {
-                list_store4<kListAuxMany>(lout, d, e);
-                wrote += 4u;
-                wsum += e.x + e.y + e.z + e.w;
-            } else {
-                report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
-            }
-        };
-        constexpr uint32_t kCopyQ = 2u;
-        for (uint32_t v0 = t; v0 < 4u * L; v0 += kCopyQ * kLineBlock) {
-            uint32_t tg[kCopyQ], sr[kCopyQ];
-#pragma unroll
-            for (uint32_t i = 0; i < kCopyQ; ++i) {
-                const uint32_t v = v0 + i * kLineBlock;
-                tg[i] = v < 4u * L ? ltag[v >> 2] : kTagSkip;
-                sr[i] = v < 4u * L ? lsrc[v >> 2] : 0u;
-            }
-#pragma unroll
-            for (uint32_t i = 0; i < kCopyQ; ++i)
-                copy_quad(v0 + i * kLineBlock, tg[i], sr[i]);
-        }
-        // the cut quads of partial lines, a thread per (bucket, quad, word)
-        for (uint32_t e = t; e < 8u * nb; e += kLineBlock) {
-            const uint32_t b = e >> 3, k = (e >> 2) & 1u, j = e & 3u;
-            const uint32_t v0 = cs[b], e1 = ve[b];
-            const uint32_t qb = (k ? e1 : v0) & ~3u, a = qb + j;
-            bool go = a >= v0 && a < e1 && ((k ? e1 : v0) & 3u) != 0u;
-            if (k == 0u)
-                go = go && !(!last && (v0 >> 4) == (e1 >> 4) && (e1 & 15u) != 0u);
-            else
-                go = go && last && !(qb == (v0 & ~3u) && (v0 & 3u) != 0u);
-            if (go) {
-                const uint32_t w = word_at(b, a, v0, ce[b], sb[b]), d = a - ph;
-                if (d < P.n) {
-                    list_store1<kListAuxMany>(lout, d, w);
-                    ++wrote;
-                    wsum += w;
-                } else {
-                    report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
-                }
-            }
-        }
-        if (!last) {
-            for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
-                const uint32_t b = e >> 4, j = e & 15u;
-                const uint32_t e1 = ve[b], v0 = cs[b], nv = max(v0, e1 & ~15u);
-                if (j < e1 - nv)
-                    cbw[e] = word_at(b, nv + j, v0, ce[b], sb[b]);
-            }
-        }
-    };
-    // the line tags of span g, and every packet of it at its stage index
-    auto place = [&](uint32_t g) {
-        const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
-        const bool last = g + 1u == g1;
-        const uint32_t sw = setk(g) * nb;
-        const uint32_t *cs = lsm + o.cs + sw, *ve = lsm + o.ve + sw, *ce = lsm + o.ce + sw;
-        const uint32_t *sb = lsm + o.sb + sw, *rb = lsm + o.rb + sw;
-        const uint32_t *lsl = lsm + o.lsl + setk(g) * (nb + 1u);
-        uint32_t *ltag = lsm + o.ltag + buf(g) * P.lmax, *lsrc = lsm + o.lsrc + buf(g) * P.lmax;
-        uint16_t *stg = reinterpret_cast<uint16_t *>(lsm + o.stg + buf(g) * o.stg_words);
-        const uint32_t *tab = lsm + o.tab + buf(g) * ntab;
-        const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + setk(g)]);
-        if (tj < tk) {
-            const uint32_t b = opaque(tb);
-            const uint32_t l0 = lsl[b], l1 = L ? min(lsl[b + 1u], L) : 0u, v0 = cs[b], e1 = ve[b];
-            const uint32_t e0 = ce[b], src0 = sb[b] - e0;
-            for (uint32_t l = l0 + tj; l < l1; l += tk) {
-                const uint32_t gl = l - l0 + (v0 >> 4), a = 16u * gl;
-                const uint32_t tag = b | (a >= v0 && a + 16u <= e1 ? 0u
-                                          : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u
-                                              ? kTagSkip
-                                              : kTagPartial) |
-                                     (a < e0 ? kTagCarried : 0u);
-                ltag[l] = tag;
-                lsrc[l] = src0 + a;
-            }
-        }
-        // a group at a time: every slot of it read before any stage write
-        // (the thread index hidden from the optimiser: its 32 packet offsets
-        // were hoisted out of the phase loop and spilled)
-        const uint32_t tt = opaque(t);
-#pragma unroll
-        for (uint32_t k0 = 0; k0 < kWideG; k0 += 1u) {
-            uint32_t slot[1][8];
-#pragma unroll
-            for (uint32_t k = k0; k < k0 + 1u; ++k) {
-                const uint32_t o8 = 8u * (k * kLineBlock + tt);
-                const uint32_t cc = min(o8 >> P.cshift, ncs - 1u);
-#pragma unroll
-                for (uint32_t j = 0; j < 8u; ++j) {
-                    const uint32_t rk = (pk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu;
-                    const uint32_t b = bucket_of(
-                        (int16_t)((qk[k][j >> 1] >> (16u * (j & 1u))) & 0xffffu), P.nq);
-                    slot[k - k0][j] = tab[(b << P.gshift) + cc] + rb[b] + rk;
-                }
-            }
-#pragma unroll
-            for (uint32_t k = k0; k < k0 + 1u; ++k) {
-                const uint32_t o8 = 8u * (k * kLineBlock + tt);
-#pragma unroll
-                for (uint32_t j = 0; j < 8u; ++j)
-                    if (len == kWideSpan || o8 + j < len)
-                        stg[min(slot[k - k0][j], cap)] = (uint16_t)(o8 + j);
-            }
-        }
-    };
-    // phase c - g0: span c + 1's loads; span c - 1 out; span c placed; wait;
-    // span c + 1 laid out and its table written; the barrier
-    for (uint32_t c = g0; c <= g1; ++c) {
-        const uint32_t g = c;   // (the phase clock's span index)
-        (void)g;
-        LPROF(0);
-        const bool more = c + 1u < g1;
-        if (copier) {
-            if (c > g0)
-                copy_out(c - 1u);
-        } else {
-            // span c placed, then span c + 1's streams loaded into the same
-            // registers (one set: 128 VGPRs at 16 waves a CU); their latency
-            // overlaps the copy-out waves' stores
-            if (c < g1)
-                place(c);
-            if (more)
-                load_span(c + 1u, pk, qk);
-            LPROF(2);
-            __builtin_amdgcn_s_waitcnt(kWaitVm0);
-            LPROF(3);
-            if (more) {
-                if (wave == 0)
-                    layout(c + 1u);
-                write_tab(c + 1u);
-            }
-            LPROF(4);
-        }
-        __syncthreads();
-        LPROF(5);
-    }
     wrote = __shfl(wave_incl_scan(wrote, lane), kWave - 1, kWave);
     wsum = __shfl(wave_incl_scan(wsum, lane), kWave - 1, kWave);
     if (lane == 0) {
@@ -3286,7 +2772,6 @@ struct yrss_ctx {
         uint64_t worker_inject = 0;   // ticket whose worker burst fires a list guard
         uint32_t line_groups = 0;     // force the line scatter's kG (2 or 4)
         uint32_t skip_line_check = 0; // launch a line scatter the host check refuses
-        uint32_t line_desync = 0;     // odd line-scatter workgroups start late (100 MHz ticks)
         uint32_t partial_merge = 0;   // partial list lines as plain stores
     } dbg;
 };
@@ -3405,8 +2890,7 @@ ScatterLds scatter_lds(uint32_t nb)
 // than a span can be (batches past ~2^29 packets) or the LDS would not fit.
 struct LinePlan {
     bool ok, packed;
-    bool fits;   // nb within the kernel's per-bucket capacity (line_nb_max, kWideNbMax)
-    bool wide;   // yrss_scatter_wide (past 128 buckets), else yrss_scatter_lines<kG>
+    bool fits;   // nb within the kernel's per-bucket capacity (line_nb_max)
     uint32_t groups, gshift, seg, lmax, lds;
 };
 
@@ -3414,16 +2898,11 @@ LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
 {
     LinePlan p{};
     const uint32_t nb = c->nb, cshift = lay.ct_shift + 6u;
-    // kG = 2 up to 128 buckets, 4 past that; the test hook forces a kernel:
-    // 1 the pipelined yrss_scatter_wide (measured slower),
-    // 2 / 4 yrss_scatter_lines<kG>
-    const uint32_t force = c->dbg.line_groups;
-    p.wide = force == 1u;
-    p.groups = p.wide ? kWideG : force ? force : nb > line_nb_max(2) ? 4u : 2u;
-    p.fits = (p.wide ? nb <= kWideNbMax : nb <= line_nb_max(p.groups)) &&
-             nb <= (uint32_t)kLineBlock;
-    const uint32_t smax = p.wide ? kWideSpan : line_span_max(p.groups);
-    const uint32_t tmax = p.wide ? kWideTabMax : line_tab_max(p.groups);
+    // kG = 2 up to 128 buckets, 4 past that (the test hook forces one)
+    p.groups = c->dbg.line_groups ? c->dbg.line_groups : nb > line_nb_max(2) ? 4u : 2u;
+    p.fits = nb <= line_nb_max(p.groups) && nb <= (uint32_t)kLineBlock;
+    const uint32_t smax = line_span_max(p.groups);
+    const uint32_t tmax = line_tab_max(p.groups);
     if (lay.chunk > smax || nb > (uint32_t)kLineBlock)
         return p;
     uint64_t target = c->tune.span_tiles ? (uint64_t)c->tune.span_tiles * kTile : smax;
@@ -3436,12 +2915,11 @@ LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
         return p;
     p.seg = lay.chunk << p.gshift;
     p.lmax = p.seg / 16u + 2u * nb + 1u;   // a bucket's lines <= (its packets + 30) / 16
-    p.lds = (p.wide ? wide_lds(nb, p.gshift, p.lmax, p.seg).words
-                    : line_lds(nb, p.gshift, p.lmax).words) * 4u;
+    p.lds = line_lds(nb, p.gshift, p.lmax).words * 4u;
     if (p.lds > 160u * 1024u)
         return p;
-    // bucket << cshift | rank fits 16 bits (the wide kernel always reads q)
-    p.packed = !p.wide && cshift < 16u && nb <= (1u << (16u - cshift));
+    // bucket << cshift | rank fits 16 bits
+    p.packed = cshift < 16u && nb <= (1u << (16u - cshift));
     p.ok = true;
     return p;
 }
@@ -4316,19 +3794,18 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         S.xcd = c->tune.scatter_xcd != 0 ? 1u : 0u;
         S.nt = c->nb > kListNtBuckets ? 1u : 0u;
         S.early = c->nb > 16u ? 1u : 0u;
-        S.desync = c->dbg.line_desync;
         S.merge = c->dbg.partial_merge;
         // persistent: the resident workgroups, each one contiguous range of
         // spans, never more workgroups than spans
         const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
         void (*fn)(LineParams) =
-            lp.wide ? yrss_scatter_wide
-            : lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
-                              : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
-        const uint32_t blk = lp.wide ? (uint32_t)kWideBlock : (uint32_t)kLineBlock;
-        const uint32_t sgrid = std::min(spans, resident_blocks(c, (const void *)fn, blk, lp.lds));
+            lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
+                            : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
+        const uint32_t sgrid =
+            std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
         Timed t(c, YRSS_K_SCATTER);
-        hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(blk), lp.lds, s, t.a, t.b, 0, S);
+        hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(kLineBlock), lp.lds, s, t.a,
+                              t.b, 0, S);
         YRSS_HIP(hipGetLastError());
         return 0;
     }
@@ -5400,7 +4877,7 @@ int yrss_debug_worker_inject(yrss_ctx *c, uint64_t ticket)
 
 int yrss_debug_line_groups(yrss_ctx *c, uint32_t groups, int skip_host_check)
 {
-    if (!c || groups > 4u || groups == 3u || skip_host_check < 0 ||
+    if (!c || (groups != 0u && groups != 2u && groups != 4u) || skip_host_check < 0 ||
         skip_host_check > 1)
         return -EINVAL;
     c->dbg.line_groups = groups;
@@ -5416,13 +4893,6 @@ int yrss_debug_partial_merge(yrss_ctx *c, int on)
     return 0;
 }
 
-int yrss_debug_line_desync(yrss_ctx *c, uint32_t ticks)
-{
-    if (!c || ticks > 100000u)   // <= 1 ms
-        return -EINVAL;
-    c->dbg.line_desync = ticks;
-    return 0;
-}
 #endif
 
 int yrss_timing_enable(yrss_ctx *c, int enable)
