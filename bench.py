@@ -554,18 +554,29 @@ def pcie_inclusive(profile: str, place=None):
     # best counts of the sweeps), ring depth 4 x workgroups.
     # Three runs each (median, spread), every run with its host cycles per
     # burst and the thread's and pool's NUMA placement beside the GPU's.
-    for frames, burst, blocks in (("0", 32, 128), ("0", 1024, 32), ("1", 32, 128),
-                                  ("1", 1024, 32), ("2", 32, 128), ("2", 1024, 32)):
-        print(f"pcie_inclusive: worker form {frames}, burst {burst}", file=sys.stderr, flush=True)
+    # Pools: 2^20 mbufs (2.4 GB, cache-cold: every header and window a DRAM
+    # miss), and 16384 mbufs, whose touched lines (4 MB) stay LLC-resident as
+    # an rx ring's recycled mbufs do after rte_eth_rx_burst.  The windows
+    # form's staging copy is non-temporal at 1024-packet bursts (+14 % on the
+    # cold pool, no read-for-ownership of lines the GPU read), plain at 32
+    # (profiles/r05_windows_copy_ab.log).
+    rows = (("0", 32, 128, 1 << 20, 0), ("0", 1024, 32, 1 << 20, 0),
+            ("1", 32, 128, 1 << 20, 0), ("1", 1024, 32, 1 << 20, 0),
+            ("2", 32, 128, 1 << 20, 0), ("2", 1024, 32, 1 << 20, 1),
+            ("1", 32, 128, 16384, 0), ("2", 32, 128, 16384, 0))
+    for frames, burst, blocks, pool, win_nt in rows:
+        print(f"pcie_inclusive: worker form {frames}, burst {burst}, pool {pool}", file=sys.stderr,
+              flush=True)
         try:
-            r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
+            r = subprocess.run([str(exe), str(PROFILES[profile]), str(pool), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
                                env={**os.environ, **pin, "YRSS_CBENCH_MODES": "4",
                                     "YRSS_CBENCH_REPEAT": "3",
                                     "YRSS_CBENCH_WORKER_DEPTH": str(4 * blocks),
                                     "YRSS_CBENCH_WORKER_BLOCKS": str(blocks),
                                     "YRSS_CBENCH_WORKER_SLOTOUT": "1",
-                                    "YRSS_CBENCH_WORKER_FRAMES": frames})
+                                    "YRSS_CBENCH_WORKER_FRAMES": frames,
+                                    "YRSS_CBENCH_WIN_NT": str(win_nt)})
         except subprocess.TimeoutExpired:
             break
         lines = []
@@ -580,7 +591,9 @@ def pcie_inclusive(profile: str, place=None):
         rd = {"0": 136, "1": 74, "2": 66}[frames]
         for row in _cbench_rows(lines, ("api", "burst", "inflight", "blocks", "note")):
             gbs = row["mpps"] * 1e6 * (rd + 10) / 1e9
-            row.update({"link_bytes_per_pkt": rd + 10, "link_GBps": round(gbs, 2),
+            row.update({"pool_mbufs": pool, "pool": "cold" if pool > (1 << 16) else "llc",
+                        "staging_nt": bool(win_nt) if frames == "2" else None,
+                        "link_bytes_per_pkt": rd + 10, "link_GBps": round(gbs, 2),
                         "link_frac": round(gbs / PCIE_GEN5_X16_GBS, 4),
                         "gpu_node": place.get("gpu_node"),
                         "dispatch_cpu": place.get("dispatch_cpu"),
