@@ -44,7 +44,7 @@ def test_shipping_library_has_no_test_or_measurement_paths():
     assert sorted(re.findall(r"\bT (yrss_debug_\w+)", test)) == hooks
     # the measurement macro refuses a product build
     src = (abi.REPO_DIR / "yastack_amd" / "csrc" / "yrss.hip").read_text()
-    assert "#if defined(YRSS_PROF_LINES) && !defined(YRSS_TOOLS_BUILD)\n#error" in src
+    assert "!defined(YRSS_TOOLS_BUILD)\n#error" in src
     assert "YRSS_NO_CNT_FLUSH" not in src and "getenv(\"YRSS_WORKER_INJECT\")" not in src
 
 

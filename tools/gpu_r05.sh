@@ -95,6 +95,19 @@ merge)
     step winab 600 python tools/win_ab.py --pools 1048576,16384 || exit 1
     cat gpurun_out/ab.log gpurun_out/winab.log
     ;;
+abl)
+    : > gpurun_out/lineprof_abl.log
+    vs=("base -DYRSS_ABL_NONE=1" "nostore -DYRSS_ABL_NOSTORE=1" "noload -DYRSS_ABL_NOLOAD=1")
+    [ -n "${ABL_ONLY:-}" ] && vs=("base -DYRSS_ABL_NONE=1")
+    for v in "${vs[@]}"; do
+        set -- $v
+        tools/build_ab_lib.sh prof_$1 -DYRSS_PROF_LINES=1 $2 > gpurun_out/build_$1.log 2>&1 || exit 1
+        echo "== $1" >> gpurun_out/lineprof_abl.log
+        timeout -k 10 200 python tools/line_prof.py --lib ab/lib/libyrss_prof_$1.so \
+            --nb-procs 64,255 >> gpurun_out/lineprof_abl.log 2>&1 || exit 1
+    done
+    cat gpurun_out/lineprof_abl.log
+    ;;
 prof)
     # the line scatter's phase clock (a tools build with the test hooks)
     tools/build_ab_lib.sh prof -DYRSS_PROF_LINES=1 -DYRSS_TEST_HOOKS=1 > gpurun_out/build_prof.log 2>&1 || exit 1

@@ -79,13 +79,18 @@ def main() -> int:
         print(f"   span total mean {per_span.mean():.0f} ns")
         # slots 7 / 6 of span 0: kernel entry and the look-back's end
         entry = p[:, 0, 7][used[:, 0]]
-        lbend = p[:, 0, 6][used[:, 0]]
+        # slot 6: wave 0 done laying out the next span (inside phase c)
+        lay = (p[:, :, 6] - p[:, :, 3])[used & (p[:, :, 6] != 0)] * 10
+        if lay.size:
+            print(f"   wave 0's layout of the next span (in c) mean {lay.mean():.0f} ns  "
+                  f"p90 {np.percentile(lay, 90):.0f}")
+        lbend = np.zeros(0)
         if (entry > 0).all():
             k0 = entry.min()
             pro = (first - entry) * 10
             print(f"   entry spread {(entry.max() - k0) * 10:.0f} ns; entry -> first span mean "
                   f"{pro.mean():.0f} p90 {np.percentile(pro, 90):.0f} ns")
-            if (lbend > 0).all():
+            if lbend.size and (lbend > 0).all():
                 print(f"   entry -> look-back done mean {((lbend - entry) * 10).mean():.0f} ns")
             endk = (ends - k0) * 10
             ids = np.nonzero(used[:, 0])[0]

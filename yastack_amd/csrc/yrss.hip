@@ -1308,8 +1308,9 @@ __device__ __forceinline__ void load_groups(const uint16_t *a, uint32_t p0, uint
     }
 }
 
-#if defined(YRSS_PROF_LINES) && !defined(YRSS_TOOLS_BUILD)
-#error "YRSS_PROF_LINES is a measurement build: tools/build_ab_lib.sh only, never libyrss.so"
+#if (defined(YRSS_PROF_LINES) || defined(YRSS_ABL_NOSTORE) || defined(YRSS_ABL_NOLOAD)) && \
+    !defined(YRSS_TOOLS_BUILD)
+#error "YRSS_PROF_LINES / YRSS_ABL_* are measurement builds: tools/build_ab_lib.sh only"
 #endif
 #ifdef YRSS_PROF_LINES
 // measurement builds only (tools/line_prof.py): per workgroup and span, the
@@ -1604,8 +1605,18 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         //   reads; a wave per bucket walked nb / 8 buckets in turn);
         // - the carried words into their stage slots;
         // - every packet at slot = tab[b][chunk] + rank.
+#ifdef YRSS_ABL_NOLOAD   // measurement builds only: no next-span stream loads
+        if (!last) {
+#pragma unroll
+            for (uint32_t k = 0; k < kG; ++k) {
+                pkn[k] = pk[k];
+                qkn[k] = qk[k];
+            }
+        }
+#else
         if (!last)
             load_span(g + 1u, pkn, qkn);
+#endif
         if (tj < tk) {
             const uint32_t b = opaque(tb);   // (addresses not hoisted: registers)
             // (bounded by the span's line count whatever the words say)
@@ -1685,6 +1696,9 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             if (mode == 0u) {
                 const uint32_t d = a0 - ph;
                 if (d + 4u <= P.n && d + 4u > d) {
+#ifdef YRSS_ABL_NOSTORE   // measurement builds only: the copy-out without its stores
+                    if (e.x == 0xffffffffu)
+#endif
                     if (P.nt)
                         list_store4<kListAuxMany>(lout, d, e);
                     else
@@ -1728,6 +1742,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         constexpr uint32_t kCopyQ = 5u, nct = kLineBlock;
         if (!last && wave == 0)
             layout(g + 1u, s ^ 1u);
+        LPROF(6);
         for (uint32_t v0 = t; v0 < 4u * L; v0 += kCopyQ * nct) {
             uint32_t tg[kCopyQ], gl[kCopyQ];
             u32x4 eq[kCopyQ];
