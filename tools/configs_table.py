@@ -48,7 +48,7 @@ def main():
     for cid, prof, desc, extra in CONFIGS + (QUEUES if args.queues else []):
         cmd = [sys.executable, str(ROOT / "bench.py"), "--profile", prof, "--steps",
                str(args.steps), "--cpu-seconds", str(args.cpu_seconds if not extra else 0),
-               "--pcie", "0", *extra]
+               "--pcie", "0", "--extra-configs=", *extra]
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
         line = next((ln for ln in r.stdout.splitlines() if ln.startswith("{")), None)
         if r.returncode != 0 or line is None:

@@ -23,4 +23,8 @@ d = json.loads(sys.stdin.read())
 c = d["check"]
 print(json.dumps({"n_gpus": d["n_gpus"], "profile": d["config"]["workload"], "value": d["value"],
                   "ms_per_step": d["ms_per_step"], "ranks_checked": c["ranks_checked"],
-                  "bit_exact": c["bit_exact"], "cpu_baseline": d["cpu_baseline"] is not None}))'
+                  "bit_exact": c["bit_exact"], "cpu_baseline": d["cpu_baseline"] is not None}))
+for x in d.get("configs_extra") or []:
+    print(json.dumps({k: x[k] for k in ("config", "profile", "n_gpus", "value", "ms_per_step",
+                                        "parse_us", "roofline_frac", "ranks_checked",
+                                        "bit_exact")}))'
