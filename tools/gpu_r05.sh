@@ -108,6 +108,13 @@ abl)
     done
     cat gpurun_out/lineprof_abl.log
     ;;
+carry)
+    step tests 600 python -u -m pytest tests/test_gpu_layout.py tests/test_gpu_small_burst.py -x -q \
+        --timeout 120 --timeout-method thread || exit 1
+    step ab 1200 python tools/ab_inproc.py --nb-procs "${AB_Q:-8,64,255}" \
+        --libs "cur,ablib/libyrss_r05base.so" --rounds "${AB_ROUNDS:-6}" || exit 1
+    cat gpurun_out/ab.log
+    ;;
 prof)
     # the line scatter's phase clock (a tools build with the test hooks)
     tools/build_ab_lib.sh prof -DYRSS_PROF_LINES=1 -DYRSS_TEST_HOOKS=1 > gpurun_out/build_prof.log 2>&1 || exit 1

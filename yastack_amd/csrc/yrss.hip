@@ -1530,6 +1530,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         uint32_t *wcs = cs + s * nb, *wve = ve + s * nb, *wce = ce + s * nb, *wso = so + s * nb;
         uint32_t *wrb = rb + s * nb, *wlsl = lsl + s * (nb + 1u);
         uint32_t lines = 0;
+        bool cut = false;   // a bucket's first valid position not on a quad: cut quads
         // (lane hidden from the optimiser: the per-lane LDS addresses of
         // both sets were hoisted out of the span loop and spilled)
         const uint32_t ll = opaque(lane);
@@ -1556,6 +1557,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 wrb[b] = 16u * (l0 - (v0 >> 4)) + e0 - w0s[i];
             }
             lines += __shfl(x, kWave - 1, kWave);
+            cut |= __ballot(b < nb && (v0 & 3u) != 0u) != 0ull;
         }
         if (lane == 0) {
             if (lines > P.lmax) {
@@ -1564,6 +1566,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             }
             wlsl[nb] = lines;
             misc[4u + s] = lines;
+            misc[6u + s] = cut ? 1u : 0u;
         }
     };
     __syncthreads();   // set 1 written
@@ -1630,10 +1633,23 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 lgl[l] = gl;
             }
         }
-        for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
-            const uint32_t b = e >> 4, j = e & 15u;
-            if (j < ce[b] - cs[b])
-                stg[min(so[b] + cs[b] + j, cap)] = cb[e];
+        // the carried words, a quad a thread (a 16-byte copy where the quad
+        // is whole and its stage slots aligned, else word by word: a whole-quad
+        // write past ce would race the placement of the span's own packets)
+        for (uint32_t e = t; e < 4u * nb; e += kLineBlock) {
+            const uint32_t b = e >> 2, q4 = 4u * (e & 3u);
+            const uint32_t n = ce[b] - cs[b], base = so[b] + cs[b];
+            if (q4 >= n)
+                continue;
+            if (q4 + 4u <= n && ((base + q4) & 3u) == 0u && base + q4 + 4u <= cap) {
+                reinterpret_cast<u32x4 *>(stg)[(base + q4) >> 2] =
+                    reinterpret_cast<const u32x4 *>(cb)[4u * b + (q4 >> 2)];
+            } else {
+#pragma unroll
+                for (uint32_t j = 0; j < 4u; ++j)
+                    if (q4 + j < n)
+                        stg[min(base + q4 + j, cap)] = cb[16u * b + q4 + j];
+            }
         }
         // (a packed bucket past nb reads some other LDS word as its slot
         // base: the slot is clamped and the hole it leaves is reported)
@@ -1769,7 +1785,11 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         // a lane, from the stage: a wave-instruction stores 64 such words
         // where the copy-out's per-quad word stores cost four
         // wave-instructions for every turn that held one
-        for (uint32_t e = t; e < 8u * nb; e += kLineBlock) {
+        // (only the range's last span can cut an end; a start is cut only
+        // while some bucket's first valid position is off a quad: layout
+        // records that, so a middle span usually skips the pass)
+        const uint32_t ncut = last || misc[6u + s] ? 8u * nb : 0u;
+        for (uint32_t e = t; e < ncut; e += kLineBlock) {
             const uint32_t b = e >> 3, k = (e >> 2) & 1u, j = e & 3u;
             const uint32_t v0 = cs[b], e1 = ve[b];
             const uint32_t qb = (k ? e1 : v0) & ~3u, a = qb + j;
@@ -1798,11 +1818,24 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         LPROF(4);
         // (d) carry the unfinished last lines
         if (!last) {
-            for (uint32_t e = t; e < 16u * nb; e += kLineBlock) {
-                const uint32_t b = e >> 4, j = e & 15u;
+            // a quad a thread: a 16-byte copy where the stage slots are
+            // aligned (the words past the end carry nothing the next span
+            // reads), else word by word
+            for (uint32_t e = t; e < 4u * nb; e += kLineBlock) {
+                const uint32_t b = e >> 2, q4 = 4u * (e & 3u);
                 const uint32_t e1 = ve[b], nv = max(cs[b], e1 & ~15u);
-                if (j < e1 - nv)
-                    cb[e] = stg[min(so[b] + nv + j, cap)];
+                const uint32_t n = e1 - nv, base = so[b] + nv;
+                if (q4 >= n)
+                    continue;
+                if (((base + q4) & 3u) == 0u && base + q4 <= cap) {
+                    reinterpret_cast<u32x4 *>(cb)[4u * b + (q4 >> 2)] =
+                        reinterpret_cast<const u32x4 *>(stg)[(base + q4) >> 2];
+                } else {
+#pragma unroll
+                    for (uint32_t j = 0; j < 4u; ++j)
+                        if (q4 + j < n)
+                            cb[16u * b + q4 + j] = stg[min(base + q4 + j, cap)];
+                }
             }
             // the next span's (a) rewrites the per-bucket arrays read above
             __syncthreads();
