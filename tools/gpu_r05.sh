@@ -41,7 +41,7 @@ wide1)
         --timeout-method thread -k "many_bucket or forced_line or capacity or bucket_counts" || exit 1
     step pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit 1
     step ab 900 python tools/ab_inproc.py --nb-procs "${AB_Q:-3,64,129,255}" \
-        --libs "cur,ablib/libyrss_r05base.so" --rounds "${AB_ROUNDS:-6}" || exit 1
+        --libs "cur,${AB_BASE:-ablib/libyrss_r05base.so}" --rounds "${AB_ROUNDS:-6}" || exit 1
     step winab 600 python tools/win_ab.py || exit 1
     # write bytes: the bare list-write pattern, then the scatter at 255 queues
     for nb in 64 256; do
@@ -112,7 +112,7 @@ carry)
     step tests 600 python -u -m pytest tests/test_gpu_layout.py tests/test_gpu_small_burst.py -x -q \
         --timeout 120 --timeout-method thread || exit 1
     step ab 1200 python tools/ab_inproc.py --nb-procs "${AB_Q:-8,64,255}" \
-        --libs "cur,ablib/libyrss_r05base.so" --rounds "${AB_ROUNDS:-6}" || exit 1
+        --libs "cur,${AB_BASE:-ablib/libyrss_r05base.so}" --rounds "${AB_ROUNDS:-6}" || exit 1
     cat gpurun_out/ab.log
     ;;
 prof)

@@ -1353,7 +1353,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     uint32_t *lgl = lsm + o.lgl;
     uint32_t *stg = lsm + o.stg;
     uint32_t *const cs_sets = cs, *const ve_sets = ve, *const ce_sets = ce, *const so_sets = so;
-    uint32_t *const rb_sets = rb, *const lsl_sets = lsl;
+    uint32_t *const lsl_sets = lsl;
     const uint32_t cap = 16u * P.lmax;   // the spare word
     // list position x is "adjusted" a = x + ph: 64-byte lines are a >> 4
     const uint32_t ph = (uint32_t)(((uintptr_t)P.qidx >> 2) & 15u);
@@ -1395,10 +1395,10 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     uint32_t pt[kLineTabRegs], w0s[kBI], w0e[kBI];
     auto load_span = [&](uint32_t g, u32x4 (&pk)[kG], u32x4 (&qk)[kG]) {
         const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
-        load_groups(P.rank, p0, pe, tt, pk);
-        if (!kPacked)
-            load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, qk);
         const uint32_t c0 = g << P.gshift;
+        // the prefixes first, the streams last: vmcnt counts in issue order,
+        // so the prologue can wait for the prefixes alone (the first span's
+        // layout and table then overlap its streams' arrival)
         if (wave == 0) {
             // rows past nb read 0 (range check); a span's end past the last
             // chunk is the bucket's total
@@ -1437,25 +1437,31 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             if (k * kLineBlock < ntab)   // (uniform)
                 pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo,
                                                              (int)(c0 * 4u + k * step), 0);
+        load_groups(P.rank, p0, pe, tt, pk);
+        if (!kPacked)
+            load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, qk);
     };
-    // Past 16 buckets the first span's streams and prefixes are issued before
-    // the totals are read, so the two round trips overlap (such batches are
-    // rarely one-list, where these loads go unused)
-    if (P.early && g0 < g1) {
-        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
-        load_span(g0, pkA, qkA);
-    }
     // list starts (exclusive scan of totals); workgroup 0 also writes qstart.
     // Every bucket block's total is loaded before the first is scanned: one
-    // round trip, not one per 64 buckets.
+    // round trip, not one per 64 buckets.  The totals go first: waiting for
+    // them must not wait for the first span's streams behind them.
+    constexpr uint32_t kTB = line_bucket_regs(kG);   // nb <= 64 kTB (checked at entry)
+    uint32_t tv[kTB];
     if (wave == 0) {
-        constexpr uint32_t kTB = line_bucket_regs(kG);   // nb <= 64 kTB (checked at entry)
-        uint32_t tv[kTB];
 #pragma unroll
         for (uint32_t i = 0; i < kTB; ++i) {
             const uint32_t b = i * kWave + lane;
             tv[i] = i * kWave < nb && b < nb ? P.totals[b] : 0u;
         }
+    }
+    // Past 16 buckets the first span's prefixes and streams are issued before
+    // the totals are scanned, so the round trips overlap (such batches are
+    // rarely one-list, where these loads go unused)
+    if (P.early && g0 < g1) {
+        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
+        load_span(g0, pkA, qkA);
+    }
+    if (wave == 0) {
         uint32_t carry = 0, nzb = 0;
 #pragma unroll
         for (uint32_t i = 0; i < kTB; ++i) {
@@ -1509,11 +1515,10 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
         load_span(g0, pkA, qkA);
     }
-    // the first span's loads waited for here, so that at the loop head no
-    // load is pending on any path: a pending one there made the compiler wait
-    // vmcnt(0) at the prefix table's first use in every span, i.e. for the
-    // previous span's list stores as well
-    __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    // the first span's prefixes waited for here, its streams (issued last,
+    // kG 16-byte loads a stream, more on a ragged span) left in flight under
+    // the first layout and table
+    __builtin_amdgcn_s_waitcnt(kWaitVm0 | (int)(kPacked ? kG : 2u * kG));
     if (t < nb) {
         const uint32_t a = start[t] + pre0 + ph;
         cs[nb + t] = a;
@@ -1569,9 +1574,28 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             misc[6u + s] = cut ? 1u : 0u;
         }
     };
+    // span g's prefix table, tab[b][c] = prefix at chunk c + rb[b] (rows of
+    // ncs + 1 words, every thread its prefix words pt): a packet's stage slot
+    // is then tab[b][chunk] + rank
+    auto write_tab = [&](uint32_t s) {
+        const uint32_t *rbs = rb + s * nb;
+        const uint32_t tt = opaque(t);   // (addresses not hoisted out of the span loop: spills)
+#pragma unroll
+        for (uint32_t k = 0; k < kLineTabRegs; ++k) {
+            const uint32_t e = k * kLineBlock + tt;
+            if (k * kLineBlock < ntab && e < ntab)
+                tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k] + rbs[e >> P.gshift];
+        }
+    };
     __syncthreads();   // set 1 written
     if (wave == 0)
         layout(g0, 0u);
+    __syncthreads();
+    write_tab(0u);
+    // nothing pending at the loop head: a pending load there made the
+    // compiler wait vmcnt(0) at a first use in every span, i.e. for the
+    // previous span's list stores as well
+    __builtin_amdgcn_s_waitcnt(kWaitVm0);
     __syncthreads();
     // words written and their sum: a range is complete iff it wrote each of
     // its packets once, so the sum must be that of its packet indices (two
@@ -1584,19 +1608,11 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
         const bool last = g + 1u == g1;
         const uint32_t *cs = cs_sets + s * nb, *ve = ve_sets + s * nb, *ce = ce_sets + s * nb;
-        const uint32_t *so = so_sets + s * nb, *rb = rb_sets + s * nb;
+        const uint32_t *so = so_sets + s * nb;
         const uint32_t *lsl = lsl_sets + s * (nb + 1u);
         LPROF(0);
-        // (a) every thread: its prefix words into the table with their row's
-        // bias, tab[b][c] = prefix at chunk c + rb[b] (rows of ncs + 1
-        // words): a packet's stage slot is then tab[b][chunk] + rank
-#pragma unroll
-        for (uint32_t k = 0; k < kLineTabRegs; ++k) {
-            const uint32_t e = k * kLineBlock + t;
-            if (k * kLineBlock < ntab && e < ntab)
-                tab[(e >> P.gshift) * rs + (e & (ncs - 1u))] = pt[k] + rb[e >> P.gshift];
-        }
-        __syncthreads();
+        // (the table was written in the previous span's copy-out, or the
+        // prologue: two barriers a span)
         LPROF(1);
         const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + s]);
         // (b) three independent writes into LDS, no barrier between them:
@@ -1699,8 +1715,13 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         LPROF(2);
         // the next span's streams and prefixes (issued in (b)) have arrived;
         // waiting here, before this span's list stores, keeps those stores
-        // out of the next wait (vmcnt counts loads and stores in one queue)
+        // out of the next wait (vmcnt counts loads and stores in one queue).
+        // Wave 0 then lays the next span out into set s ^ 1 from its
+        // prefixes (no one reads that set in this span), so after the barrier
+        // every thread can write the next span's table during the copy-out
         __builtin_amdgcn_s_waitcnt(kWaitVm0);
+        if (!last && wave == 0)
+            layout(g + 1u, s ^ 1u);
         __syncthreads();
         LPROF(3);
         // (c) copy-out, a quad per thread: whole lines as 16-byte non-temporal
@@ -1750,14 +1771,11 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             }
         };
         // kCopyQ quads a turn, all loaded before any is stored (an
-        // 8192-packet span's lines fit one turn up to ~128 buckets)
-        // Wave 0 first lays out the next span (its loads were waited for
-        // above), then takes its share of the copy-out (leaving the copy-out
-        // to the other seven waves was no faster: the copy-out is bound by
-        // the stores, profiles/r03_h9_ab_copyall.log).
+        // 8192-packet span's lines fit one turn up to ~128 buckets); the next
+        // span's table first (tab is read only in (b), before the barrier)
         constexpr uint32_t kCopyQ = 5u, nct = kLineBlock;
-        if (!last && wave == 0)
-            layout(g + 1u, s ^ 1u);
+        if (!last)
+            write_tab(s ^ 1u);
         LPROF(6);
         for (uint32_t v0 = t; v0 < 4u * L; v0 += kCopyQ * nct) {
             uint32_t tg[kCopyQ], gl[kCopyQ];
