@@ -23,7 +23,7 @@ import torch  # noqa: E402
 
 from yastack_amd import SoftRss, abi  # noqa: E402
 
-PH = ["a tab + layout + S1", "b tags/carried/place", "wait + S2", "c copy-out", "d carry"]
+PH = ["a (empty since c61ac37: the table is written in c)", "b tags/carried/place", "wait + wave-0 layout + S2", "c copy-out", "d carry"]
 
 
 def main() -> int:
@@ -79,10 +79,10 @@ def main() -> int:
         print(f"   span total mean {per_span.mean():.0f} ns")
         # slots 7 / 6 of span 0: kernel entry and the look-back's end
         entry = p[:, 0, 7][used[:, 0]]
-        # slot 6: wave 0 done laying out the next span (inside phase c)
+        # slot 6: every thread done writing the next span's table (start of phase c)
         lay = (p[:, :, 6] - p[:, :, 3])[used & (p[:, :, 6] != 0)] * 10
         if lay.size:
-            print(f"   wave 0's layout of the next span (in c) mean {lay.mean():.0f} ns  "
+            print(f"   next span's table write (start of c) mean {lay.mean():.0f} ns  "
                   f"p90 {np.percentile(lay, 90):.0f}")
         lbend = np.zeros(0)
         if (entry > 0).all():
