@@ -215,11 +215,16 @@ CPU_PROFILES = ("udp4", "tcp4")        # the headline stream, and every packet h
 CPU_VARIANTS = ("bit_serial", "table")  # toeplitz_hash as written; 12x256 byte tables
 CPU_RUNS = 3                            # timed windows per cell: median, min, max
 OVERLAP_MIN = 0.95                      # a multi-process cell below this is flagged
+# packets a process re-runs: 4 MiB of windows, LLC-resident as an rx burst's headers
+# are after DDIO (8 processes share a CCD's 32 MB L3).  2^20 packets (64 MiB) made
+# the udp4 cells a test of one core's DRAM streaming rate: 1-core medians of
+# 224-533 Mpkt/s across boxes for the same code.
+CPU_SAMPLE_PKTS = 1 << 16
 
 
 def cpu_worker(spec: str) -> int:
     """One pinned CPU-baseline process (bench.py --cpu-worker prof:variant:cpu):
-    the oracle's toeplitz_dispatch restatement over 2^20 packets of the stream,
+    the oracle's toeplitz_dispatch restatement over CPU_SAMPLE_PKTS packets of the stream,
     one call per packet, inlined or (variant suffix "_fnptr") through the
     registered-dispatcher function pointer as process_packets calls it
     (ff_dpdk_if.c:1078-1079).  Every "go START END" line on stdin runs one
@@ -231,7 +236,7 @@ def cpu_worker(spec: str) -> int:
         os.sched_setaffinity(0, {int(cpu)})     # what taskset -c does
     from oracle import oracle
 
-    n = 1 << 20
+    n = CPU_SAMPLE_PKTS
     win, lens = oracle.synth(PROFILES[prof], n, 0, SEED, NFLOWS[prof], 64)
     c = oracle.cfg(3, 3, 1, 1)                  # fs/config/config.ini knobs
     fast = variant.startswith("table")
@@ -401,7 +406,9 @@ def cpu_baseline(args, nb_queues):
         "call": "through the registered dispatcher's function pointer (process_packets, "
                 "ff_dpdk_if.c:1078-1079)",
         "value_inlined": inl["mpps"],
-        "sample": f"2^20 packets of each stream re-run over common windows of ~{secs:.2f}s "
+        "sample": f"2^{CPU_SAMPLE_PKTS.bit_length() - 1} packets of each stream (4 MiB of "
+                  "windows, LLC-resident as DDIO leaves an rx burst) re-run over common "
+                  f"windows of ~{secs:.2f}s "
                   f"(CLOCK_MONOTONIC start and end shared by every process of a cell), median "
                   f"of {CPU_RUNS} windows per cell, one toeplitz_dispatch call per packet "
                   "(oracle restatement, gcc -O2 fs/lib flags), processes pinned one per "
