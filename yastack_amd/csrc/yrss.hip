@@ -1528,8 +1528,9 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // and the prefixes it holds (w0s, w0e): the valid positions [cs, ve) =
     // the carried words and the span's packets, the bucket's stage lines
     // (exclusive scan), its stage offset so and the bias rb from a prefix to
-    // a stage slot.  Span g + 1's layout is made during span g's copy-out,
-    // so a span starts with its layout in place.
+    // a stage slot.  Span g + 1's layout is made at the end of span g's
+    // placement, as soon as its prefixes arrive, so a span starts with its
+    // layout and table in place.
     auto layout = [&](uint32_t g, uint32_t s) {
         const uint32_t *pcs = cs + (s ^ 1u) * nb, *pve = ve + (s ^ 1u) * nb;
         uint32_t *wcs = cs + s * nb, *wve = ve + s * nb, *wce = ce + s * nb, *wso = so + s * nb;
@@ -1855,7 +1856,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                             cb[16u * b + q4 + j] = stg[min(base + q4 + j, cap)];
                 }
             }
-            // the next span's (a) rewrites the per-bucket arrays read above
+            // the next span's placement overwrites the stage and tags read above
             __syncthreads();
         }
         LPROF(5);
