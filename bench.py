@@ -79,7 +79,7 @@ def parse_args(argv=None):
                     help="rocprofv3 PMC summary used for roofline.traffic")
     ap.add_argument("--tune", default="",
                     help="layout overrides for measurements, k=v[,k=v] (yrss_set_tuning "
-                         "fields: chunk_tiles, span_tiles, parse_blocks, scatter_xcd)")
+                         "fields: chunk_tiles, span_tiles, parse_blocks, scatter_xcd, scan_kernel)")
     ap.add_argument("--extra-configs", default="vlan6_tcp,jumbo_tcp4",
                     help="after the headline, each rank also classifies a --pkts shard of "
                          "these profiles (BASELINE configs[3], configs[4]: the 8-GPU "
@@ -626,8 +626,21 @@ def pcie_fanout(profile: str, world: int, place=None):
     out = []
     one = bool(os.environ.get("YRSS_BENCH_ONE_DEVICE"))   # rehearsal: N contexts, device 0
     devs = ",".join("0" if one else str(d) for d in range(world))
+    if one and world > 1:
+        # HIP maps a process's streams on one device onto GPU_MAX_HW_QUEUES
+        # (4) in-order hardware queues: N contexts' persistent workers on one
+        # device would queue behind each other there.  On N devices each
+        # context's streams have their own queues; the rehearsal gets one a
+        # stream (two a context: its stream and its worker's).
+        pin = {**pin, "GPU_MAX_HW_QUEUES": str(min(32, 2 * world + 4))}
     for frames, burst, blocks in (("1", 32, 128), ("1", 1024, 32), ("0", 32, 128)):
-        print(f"pcie_fanout: form {frames}, burst {burst}", file=sys.stderr, flush=True)
+        if one and world > 1:
+            # the N contexts' persistent workers share one GPU in the rehearsal:
+            # at most 192 of its 256 CUs in all (one 1024-thread workgroup a
+            # CU), so every context's workers are resident together
+            blocks = max(4, min(blocks, 192 // world))
+        print(f"pcie_fanout: form {frames}, burst {burst}, {blocks} workgroups a context",
+              file=sys.stderr, flush=True)
         try:
             r = subprocess.run([str(exe), str(PROFILES[profile]), str(1 << 20), str(burst), "1"],
                                capture_output=True, text=True, timeout=240,
@@ -646,6 +659,11 @@ def pcie_fanout(profile: str, world: int, place=None):
             except ValueError:
                 continue
         for row in _cbench_rows(lines, ("api", "burst", "gpus", "inflight", "blocks")):
+            # every run re-classifies the packets it covered on one context
+            # (yrss_dispatch_frames) and compares q and hash packet by packet
+            runs = [d for d in lines if d["api"] == row["api"] and d["burst"] == row["burst"]]
+            row["checked_pkts"] = sum(d.get("checked", 0) for d in runs)
+            row["mismatches"] = sum(d.get("mismatches", 0) for d in runs)
             row["gpu_node"] = place.get("gpu_node")
             row["dispatch_cpu"] = place.get("dispatch_cpu")
             row["dispatch_cpu_is_first_sibling"] = place.get("dispatch_cpu_is_first_sibling")

@@ -572,6 +572,9 @@ struct yrss_tuning {
     uint32_t one_launch;     /* batches <= 4096 packets in one launch: 0 host bursts
                                 and device batches, 1 host bursts only, 2 never      */
     int32_t  scatter_xcd;    /* XCD-contiguous scatter ranges: -1 default (on), 0, 1 */
+    uint32_t scan_kernel;    /* per-chunk list prefixes: 0 default (up to 16 buckets
+                                inside the line scatter, no scan kernel), 1 always
+                                the scan kernel                                      */
 };
 int yrss_set_tuning(yrss_ctx *ctx, const struct yrss_tuning *t);
 

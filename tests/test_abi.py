@@ -31,8 +31,8 @@ def test_shipping_library_has_no_test_or_measurement_paths():
     libyrss_test.so only, the phase clock (YRSS_PROF_LINES) only in
     tools/build_ab_lib.sh builds, and no hook reads the environment."""
     hooks = abi.header_functions(abi.REPO_DIR / "include" / "yrss_test_hooks.h")
-    assert hooks == ["yrss_debug_line_groups", "yrss_debug_partial_merge",
-                     "yrss_debug_worker_inject"]
+    assert hooks == ["yrss_debug_line_groups", "yrss_debug_lookback_polls",
+                     "yrss_debug_partial_merge", "yrss_debug_worker_inject"]
     ship = subprocess.run(["nm", "-D", "--defined-only", str(abi.LIB_PATH)],
                           capture_output=True, text=True, check=True).stdout
     assert not re.findall(r"\bT (yrss_debug_\w+)", ship)
@@ -44,7 +44,10 @@ def test_shipping_library_has_no_test_or_measurement_paths():
     assert sorted(re.findall(r"\bT (yrss_debug_\w+)", test)) == hooks
     # the measurement macro refuses a product build
     src = (abi.REPO_DIR / "yastack_amd" / "csrc" / "yrss.hip").read_text()
-    assert "!defined(YRSS_TOOLS_BUILD)\n#error" in src
+    prof = (abi.REPO_DIR / "yastack_amd" / "csrc" / "yrss_line_prof.h").read_text()
+    assert "#ifndef YRSS_TOOLS_BUILD\n#error" in prof
+    # the measurement paths live in the tools-only header, not in the product source
+    assert "YRSS_PROF_LINES" not in src and "YRSS_ABL" not in src
     assert "YRSS_NO_CNT_FLUSH" not in src and "getenv(\"YRSS_WORKER_INJECT\")" not in src
 
 

@@ -260,6 +260,48 @@ def test_partial_line_merge_parity(dev, oracle_mod, cfg):
 
 def test_tuning_rejects_bad_values(dev):
     with SoftRss(3, device=0, max_burst=0) as eng:
-        for kw in ({"chunk_tiles": 3}, {"span_tiles": 6}, {"one_launch": 3}, {"scatter_xcd": 2}):
+        for kw in ({"chunk_tiles": 3}, {"span_tiles": 6}, {"one_launch": 3}, {"scatter_xcd": 2},
+                   {"scan_kernel": 2}):
             with pytest.raises(abi.YrssError):
                 eng.set_tuning(**kw)
+
+
+@pytest.mark.parametrize("cfg", [(1, 1, 1, 0), (3, 3, 1, 1), (8, 8, 1, 0), (15, 15, 1, 0),
+                                 (16, 16, 1, 1)])
+def test_in_scatter_prefixes(dev, oracle_mod, cfg):
+    """Up to 16 buckets the line scatter makes its own list prefixes: the parse
+    kernel adds each workgroup's counts to a totals set (the previous batch's
+    scatter zeroed it), each scatter workgroup scans its range's chunk counts
+    and adds the earlier ranges' aggregates; no scan kernel runs.  The same
+    lists as the scan kernel (scan_kernel=1) batch after batch in one context,
+    the two alternating (the totals sets must stay in step), ragged sizes, and
+    layouts with one-chunk spans and many spans a workgroup; 17 buckets take
+    the scan kernel either way."""
+    with SoftRss(*cfg, device=0, max_burst=0) as eng:
+        k = 0
+        for n in (4097, 77777, (1 << 22) + 77, 1 << 24):
+            for scan in (0, 1, 0, 0):
+                eng.set_tuning(scan_kernel=scan)
+                profile = (abi.SYN_TCP4, abi.SYN_FUZZ, abi.SYN_IMIX)[k % 3]
+                check(eng, oracle_mod, cfg, profile, n, first=k * 1009)
+                k += 1
+        for chunk, span in ((1, 1), (4, 4), (1, 64)):
+            eng.set_tuning(chunk_tiles=chunk, span_tiles=span)
+            check(eng, oracle_mod, cfg, abi.SYN_FUZZ, (1 << 21) + 3, first=13)
+
+
+@pytest.mark.parametrize("polls", [0, 1])
+@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (15, 15, 1, 0)])
+def test_in_scatter_prefixes_without_lookback(dev, oracle_mod, cfg, polls):
+    """A line-scatter workgroup that does not see an earlier range's aggregate
+    within its polls sums that range's chunk counts itself (the path of a GPU
+    shared with other kernels, where an earlier workgroup may not be running
+    yet): forced through libyrss_test.so's hook, every range or most of them
+    take it, and the lists are the same."""
+    with SoftRss(*cfg, device=0, max_burst=0, lib_path=str(abi.TEST_LIB_PATH)) as eng:
+        assert eng._lib.yrss_debug_lookback_polls(eng._ctx, polls) == 0
+        for k, n in enumerate((77777, (1 << 22) + 77, 1 << 24)):
+            check(eng, oracle_mod, cfg, (abi.SYN_TCP4, abi.SYN_FUZZ, abi.SYN_IMIX)[k], n,
+                  first=k * 31)
+        assert eng._lib.yrss_debug_lookback_polls(eng._ctx, -1) == 0
+        check(eng, oracle_mod, cfg, abi.SYN_IMIX, 1 << 20, first=5)

@@ -41,6 +41,8 @@ if [ "${PART:-all}" = c ]; then
     step rehearse_n8_jumbo 620 bash tools/gpu_rehearse.sh 8 jumbo_tcp4 || exit 1
     step configs 900 python tools/configs_table.py || exit 1
     # last (a host SIGSEGV ends the call): can the host write device memory?
+    # (bar_probe is no part of build(): built here, where it runs)
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 tools/bar_probe.hip -o tools/bar_probe || exit 1
     for m in 0 1 2; do
         step bar_probe_$m 60 tools/bar_probe $m || exit 1
     done

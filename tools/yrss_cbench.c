@@ -280,7 +280,7 @@ static int run_fanout(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
         return 2;
     }
     uint32_t(*qs)[YRSS_MAX_QUEUES + 2] = calloc(inflight, sizeof(*qs));
-    uint64_t pkts = 0, issued = 0, handed = 0, t;
+    uint64_t pkts = 0, pkts_all = 0, issued = 0, handed = 0, t;
     uint32_t off = 0;
     double t0 = 0, t1 = 0;
     for (int pass = 0; pass < 2; ++pass) {          /* pass 0: warm-up */
@@ -310,6 +310,7 @@ static int run_fanout(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
             ++issued;
             off += B;
             pkts += B;
+            pkts_all += B;
             if ((issued & 63u) == 0)
                 t1 = now();
         }
@@ -322,20 +323,53 @@ static int run_fanout(const struct yrss_config *cfg0, uint8_t *mem, size_t mem_s
         ++handed;
     }
     t1 = now();
+    /* Consistency, outside the timed region: every pool position a burst
+     * covered holds that burst's q and hash; one context's yrss_dispatch_frames
+     * (itself bit-exact against the oracle in the GPU tests) classifies the
+     * same frames again and every packet is compared. */
+    const uint64_t covered = pkts_all < pool ? pkts_all : (uint64_t)(pool / B) * B;
+    uint64_t bad = 0;
+    {
+        struct yrss_config cfg = *cfg0;
+        cfg.max_burst = 4096;
+        yrss_ctx *rc_ctx = NULL;
+        int16_t *qr = malloc(4096 * sizeof(int16_t));
+        uint32_t *hr = malloc(4096 * sizeof(uint32_t));
+        if (!frames)
+            fill_frames(mbufs, pool, fdata, flen);
+        if (!qr || !hr || yrss_init(&cfg, &rc_ctx) != 0) {
+            fprintf(stderr, "fanout check setup failed\n");
+            return 2;
+        }
+        for (uint64_t a = 0; a < covered; a += 4096) {
+            const uint32_t m = covered - a < 4096 ? (uint32_t)(covered - a) : 4096u;
+            if (yrss_dispatch_frames(rc_ctx, fdata + a, flen + a, m, qr, hr, NULL, NULL) != 0) {
+                fprintf(stderr, "fanout check dispatch failed\n");
+                return 2;
+            }
+            for (uint32_t i = 0; i < m; ++i)
+                bad += qr[i] != q_all[a + i] || hr[i] != h_all[a + i];
+        }
+        yrss_fini(rc_ctx);
+        free(qr);
+        free(hr);
+    }
     printf("{\"tool\": \"yrss_cbench\", \"api\": \"%s\", \"profile\": %u, "
            "\"burst\": %u, \"gpus\": %u, \"inflight\": %llu, \"blocks\": %u, \"pkts\": %llu, "
+           "\"checked\": %llu, \"mismatches\": %llu, "
            "\"seconds\": %.3f, \"mpps\": %.2f, \"mode\": 5, \"note\": \"one dispatcher "
            "thread, bursts round-robin over %u contexts' persistent workers, handed off in "
            "submission order; %s read over PCIe\"",
            frames ? "yrss_fanout_submit_frames" : "yrss_fanout_submit", profile, B, nd,
-           (unsigned long long)inflight, blocks, (unsigned long long)pkts, t1 - t0,
+           (unsigned long long)inflight, blocks, (unsigned long long)pkts,
+           (unsigned long long)covered, (unsigned long long)bad, t1 - t0,
            pkts / (t1 - t0) / 1e6, nd, frames ? "windows" : "mbuf headers + windows");
     print_placement();
     printf("}\n");
     fflush(stdout);
     free(qs);
     yrss_fanout_fini(f);
-    return 0;
+    return bad ? 4 : 0;
 }
 
 /* The per-packet registration shim (yrss_toeplitz_dispatch through a

@@ -151,6 +151,7 @@ class Tuning(ctypes.Structure):
         ("parse_blocks", ctypes.c_uint32),
         ("one_launch", ctypes.c_uint32),
         ("scatter_xcd", ctypes.c_int32),
+        ("scan_kernel", ctypes.c_uint32),
     ]
 
 
@@ -241,6 +242,7 @@ _TEST_PROTOS = {
     "yrss_debug_worker_inject": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "yrss_debug_line_groups": (ctypes.c_int, [_vp, _u32, ctypes.c_int]),
     "yrss_debug_partial_merge": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "yrss_debug_lookback_polls": (ctypes.c_int, [_vp, ctypes.c_int]),
 }
 
 _lib = None

@@ -103,6 +103,8 @@ struct ParseParams {
     uint32_t kni_enable;
     uint32_t out16;       // full output bursts as 16-byte write-through stores (0: lane-granular)
     uint32_t rank_pack;   // kCount == 2: the rank word is bucket << (ct_shift + 6) | rank
+    uint32_t *tot_acc;    // kCount: per-bucket totals, added to (zeroed by the previous
+                          // line scatter), or null (the scan kernel sums them)
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
@@ -679,6 +681,16 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         // -6 us in one run and +3 us in another (profiles/r04_flush_policy_ab.log,
         // r04_early_flush_ab.log)
         static_assert(kBlock % kWaves == 0, "a thread keeps its wave");
+        // With tot_acc the workgroup also sums its counts per bucket (in the
+        // staging LDS, free after the loop) and adds them to the batch totals,
+        // so the line scatter needs no scan kernel in front of it
+        uint32_t *wtot = reinterpret_cast<uint32_t *>(smem + kTblBytes);
+        const bool tot = P.tot_acc != nullptr;   // (uniform)
+        if (tot) {
+            for (uint32_t e = threadIdx.x; e < P.nb; e += kBlock)
+                wtot[e] = 0u;
+            __syncthreads();
+        }
         const uint32_t w = threadIdx.x % kWaves;
         uint32_t j = 0, b = threadIdx.x / kWaves;
         while (b >= P.nb) {
@@ -687,13 +699,24 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         }
         while (j < kmax) {
             const uint32_t col = g0 + w + j * W;
-            if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords)
-                P.seg_cnt[(size_t)b * P.ncol + col] = cnt_base[w * kCntWords + j * P.nb + b];
+            if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords) {
+                const uint32_t v = cnt_base[w * kCntWords + j * P.nb + b];
+                P.seg_cnt[(size_t)b * P.ncol + col] = v;
+                if (tot && v)
+                    atomicAdd(&wtot[b], v);
+            }
             b += kBlock / kWaves;
             while (b >= P.nb) {
                 b -= P.nb;
                 ++j;
             }
+        }
+        if (tot) {
+            __syncthreads();
+            for (uint32_t e = threadIdx.x; e < P.nb; e += kBlock)
+                if (wtot[e])
+                    __hip_atomic_fetch_add(P.tot_acc + e, wtot[e], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -1225,6 +1248,16 @@ constexpr uint32_t line_span_max(uint32_t g) { return kLineBlock * 8u * g; }
 // (-EINVAL) and the kernel checks again at entry.
 constexpr uint32_t line_bucket_regs(uint32_t g) { return g == 2u ? 2u : 8u; }
 constexpr uint32_t line_nb_max(uint32_t g) { return 64u * line_bucket_regs(g); }
+// In-scatter prefixes (LineParams.fused) up to 16 buckets: the scan kernel and
+// its launch gap leave the step.  A range's nb x chunks counts are loaded in
+// kFusedRegs registers a thread; the look-back words are sized for
+// kLbMaxWgs workgroups.
+constexpr uint32_t kFusedMaxNb = 16;
+constexpr uint32_t kFusedRegs = 6;
+constexpr uint32_t kLbMaxWgs = 2048;
+// polls of an earlier range's aggregate (a round trip each, ~1 us) before the
+// workgroup sums that range's counts itself
+constexpr uint32_t kLbPolls = 24;
 static_assert(line_nb_max(4) <= (uint32_t)kLineBlock, "tagging: a thread to a bucket at least");
 
 
@@ -1244,14 +1277,25 @@ struct LineParams {
     uint32_t nt;               // list stores non-temporal only (no sc1): past 64 buckets
     uint32_t early;            // first span's loads before the totals: past 16 buckets
     uint32_t merge;            // partial lines (a range's first / last) as plain stores: L2 merges
+    // In-scatter prefixes (fused, up to kFusedMaxNb buckets): no scan kernel
+    // runs; totals are the parse kernel's sums, each workgroup scans its own
+    // range's chunk counts in LDS and adds the aggregates of the earlier ranges
+    const uint32_t *cnt;       // [nb][ncol] per-chunk counts (the parse kernel's)
+    uint32_t *tot_next;        // the totals set the next batch's parse kernel adds to: zeroed
+    unsigned long long *lb;    // [grid][nb] range aggregates: flag | epoch:31 | value:32
+    uint32_t fused, epoch;
+    uint32_t rts;              // row stride of the range table: range chunks + 1
+    uint32_t lb_polls;         // polls of an earlier range's aggregate (kLbPolls)
 };
 
 // LDS of a workgroup, in words: per-bucket arrays, the prefix table, the
-// carried lines, the stage's line tags, the stage (+ a spare word).
+// carried lines, the stage's line tags, the stage (+ a spare word); with
+// in-scatter prefixes also the range table and the range bases.
 struct LineLds {
-    uint32_t start, cs, ve, ce, so, rb, lsl, misc, tab, cb, ltag, lgl, stg, words;
+    uint32_t start, cs, ve, ce, so, rb, lsl, misc, tab, cb, ltag, lgl, stg, rt, bs, words;
 };
-__host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32_t lmax)
+__host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32_t lmax,
+                                            uint32_t rts = 0)
 {
     LineLds L;
     uint32_t o = 0;
@@ -1274,6 +1318,8 @@ __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32
     L.ltag = take(lmax);  // bucket | copy mode << 30 per stage line
     L.lgl = take(lmax);   // the line's list line (adjusted position / 16)
     L.stg = take(16u * lmax + 4u);
+    L.rt = take(nb * rts);   // [nb][rts]: the range's chunk prefixes, then its end
+    L.bs = take(rts ? nb : 0u);
     L.words = o;
     return L;
 }
@@ -1308,25 +1354,9 @@ __device__ __forceinline__ void load_groups(const uint16_t *a, uint32_t p0, uint
     }
 }
 
-#if (defined(YRSS_PROF_LINES) || defined(YRSS_ABL_NOSTORE) || defined(YRSS_ABL_NOLOAD)) && \
-    !defined(YRSS_TOOLS_BUILD)
-#error "YRSS_PROF_LINES / YRSS_ABL_* are measurement builds: tools/build_ab_lib.sh only"
-#endif
-#ifdef YRSS_PROF_LINES
-// measurement builds only (tools/line_prof.py): per workgroup and span, the
-// realtime clock at each phase boundary, read by thread 0
-__device__ uint64_t g_line_prof[2048 * 8 * 8];
-#define LPROF(k)                                                                       \
-    do {                                                                               \
-        if (t == 0 && blockIdx.x < 2048u && g - g0 < 8u)                              \
-            g_line_prof[(blockIdx.x * 8u + (g - g0)) * 8u + (k)] =                     \
-                __builtin_amdgcn_s_memrealtime();                                      \
-    } while (0)
-#else
-#define LPROF(k) \
-    do {         \
-    } while (0)
-#endif
+// the line scatter's phase clock (LPROF, LPROF_ENTRY): no-ops outside
+// measurement builds (tools/build_ab_lib.sh prof)
+#include "yrss_line_prof.h"
 
 template <bool kPacked, uint32_t kG>
 __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lines(LineParams P)
@@ -1342,11 +1372,8 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             report_fault(P.fault, YRSS_FAULT_LINE_CAPACITY, YRSS_K_SCATTER, nb, line_nb_max(kG));
         return;
     }
-    const LineLds o = line_lds(nb, P.gshift, P.lmax);
-#ifdef YRSS_PROF_LINES
-    if (t == 0 && blockIdx.x < 2048u)   // kernel entry, slot 7 of span 0
-        g_line_prof[(blockIdx.x * 8u) * 8u + 7u] = __builtin_amdgcn_s_memrealtime();
-#endif
+    const LineLds o = line_lds(nb, P.gshift, P.lmax, P.fused ? P.rts : 0u);
+    LPROF_ENTRY();
     uint32_t *start = lsm + o.start, *cs = lsm + o.cs, *ve = lsm + o.ve, *ce = lsm + o.ce;
     uint32_t *so = lsm + o.so, *rb = lsm + o.rb, *lsl = lsm + o.lsl;
     uint32_t *misc = lsm + o.misc, *tab = lsm + o.tab, *cb = lsm + o.cb, *ltag = lsm + o.ltag;
@@ -1360,7 +1387,11 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
 
     // this workgroup's range of spans
     const uint32_t nsp = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
-    const uint32_t r = xcd_block(P.xcd), G = gridDim.x;
+    // (in-scatter prefixes wait on the ranges before their own: ranges in
+    // blockIdx order, so those were dispatched first)
+    const uint32_t r = P.fused ? blockIdx.x : xcd_block(P.xcd), G = gridDim.x;
+    if (P.fused && blockIdx.x == 0 && t < nb)
+        P.tot_next[t] = 0u;   // read by no one in this kernel
     const uint32_t g0 = (uint32_t)((uint64_t)r * nsp / G);
     const uint32_t g1 = (uint32_t)((uint64_t)(r + 1u) * nsp / G);
     // prefix table rows are ncs + 1 words apart: with a power-of-two row the
@@ -1393,9 +1424,42 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     constexpr uint32_t kBI = line_bucket_regs(kG);   // nb <= 64 kBI (checked at entry)
     constexpr uint32_t kLineTabRegs = line_tab_regs(kG);
     uint32_t pt[kLineTabRegs], w0s[kBI], w0e[kBI];
-    auto load_span = [&](uint32_t g, u32x4 (&pk)[kG], u32x4 (&qk)[kG]) {
+    uint32_t crn = 0;   // in-scatter prefixes: the range's chunks (range table columns)
+    // (fused: `part` 1 the LDS prefixes only, 2 the streams only, 3 both)
+    auto load_span = [&](uint32_t g, u32x4 (&pk)[kG], u32x4 (&qk)[kG], uint32_t part = 3u) {
         const uint32_t p0 = g * P.seg, pe = span_end(g), tt = opaque(t);
         const uint32_t c0 = g << P.gshift;
+        if (P.fused && (part & 1u)) {
+            // the prefixes from the range table in LDS (written once, in the
+            // prologue); the range's last span ends at the range's end column
+            const uint32_t *rt = lsm + o.rt;
+            const uint32_t j0 = c0 - (g0 << P.gshift), je = min(j0 + ncs, crn);
+            if (wave == 0) {
+                const uint32_t ll = opaque(lane);
+#pragma unroll
+                for (uint32_t i = 0; i < kBI; ++i) {
+                    if (i * kWave < nb) {   // (uniform)
+                        const uint32_t b = min(i * kWave + ll, nb - 1u);
+                        w0s[i] = rt[b * P.rts + j0];
+                        w0e[i] = rt[b * P.rts + je];
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kLineTabRegs; ++k) {
+                const uint32_t e = min(k * kLineBlock + tt, ntab - 1u);
+                if (k * kLineBlock < ntab)   // (uniform)
+                    pt[k] = rt[(e >> P.gshift) * P.rts + j0 + (e & (ncs - 1u))];
+            }
+        }
+        if (P.fused) {
+            if (part & 2u) {
+                load_groups(P.rank, p0, pe, tt, pk);
+                if (!kPacked)
+                    load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, qk);
+            }
+            return;
+        }
         // the prefixes first, the streams last: vmcnt counts in issue order,
         // so the prologue can wait for the prefixes alone (the first span's
         // layout and table then overlap its streams' arrival)
@@ -1454,6 +1518,20 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             tv[i] = i * kWave < nb && b < nb ? P.totals[b] : 0u;
         }
     }
+    // in-scatter prefixes: the range's chunk counts are loaded beside the
+    // totals (one round trip for both; after them, so waiting for the totals
+    // does not wait for these), element i 512 + t of the range's nb x crn
+    // counts a thread (the host keeps nb x crn <= 512 kFusedRegs)
+    uint32_t cv[kFusedRegs];
+    if (P.fused) {
+        const uint32_t cr0 = g0 << P.gshift;
+        crn = g0 < g1 ? min(g1 << P.gshift, P.nchunk) - cr0 : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < kFusedRegs; ++i) {
+            const uint32_t e = i * kLineBlock + t, b = crn ? e / crn : 0u;
+            cv[i] = b < nb ? P.cnt[(size_t)b * P.ncol + cr0 + (e - b * crn)] : 0u;
+        }
+    }
     // Past 16 buckets the first span's prefixes and streams are issued before
     // the totals are scanned, so the round trips overlap (such batches are
     // rarely one-list, where these loads go unused)
@@ -1509,9 +1587,88 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         return;
     }
 
+    if (P.fused) {
+        // In-scatter prefixes.  (1) The range's chunk counts into the range
+        // table, then per bucket an exclusive scan over them (a wave to a
+        // row), the row's total at column crn; the totals are published as
+        // this range's aggregates at once.  (2) The range's base per bucket:
+        // the aggregates of every earlier range, read at once (a pair a
+        // thread; ranges in blockIdx order, so on an unshared GPU every range
+        // waited for was dispatched earlier).
+        // (3) base added to every column.  Every span's prefixes then come
+        // from LDS.  No workgroup waits without bound: an aggregate that does
+        // not appear within lb_polls polls is summed from the counts instead.
+        uint32_t *rt = lsm + o.rt, *bs = lsm + o.bs;
+        // the first span's streams ride under the range scan and the look-back
+        if (g0 < g1)
+            load_span(g0, pkA, qkA, 2u);
+#pragma unroll
+        for (uint32_t i = 0; i < kFusedRegs; ++i) {
+            const uint32_t e = i * kLineBlock + t, b = crn ? e / crn : 0u;
+            if (b < nb)
+                rt[b * P.rts + (e - b * crn)] = cv[i];
+        }
+        if (t < nb)
+            bs[t] = 0u;
+        __syncthreads();
+        for (uint32_t b = wave; b < nb; b += kLineBlock / kWave) {
+            uint32_t carry = 0;
+            for (uint32_t j0 = 0; j0 < crn; j0 += kWave) {
+                const uint32_t j = j0 + lane;
+                const uint32_t x = j < crn ? rt[b * P.rts + j] : 0u;
+                const uint32_t s = wave_incl_scan(x, lane);
+                if (j < crn)
+                    rt[b * P.rts + j] = carry + s - x;
+                carry += __shfl(s, kWave - 1, kWave);
+            }
+            if (lane == 0) {
+                rt[b * P.rts + crn] = carry;
+                __hip_atomic_store(P.lb + (size_t)r * nb + b, scan_status(P.epoch, false, carry),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        for (uint32_t e = t; e < r * nb; e += kLineBlock) {
+            const uint32_t rr = e / nb, b = e - rr * nb;
+            uint32_t v = 0;
+            bool got = false;
+            for (uint32_t polls = 0; polls < P.lb_polls; ++polls) {
+                const unsigned long long w =
+                    __hip_atomic_load(P.lb + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)((w >> 32) & 0x7fffffffu) == (P.epoch & 0x7fffffffu)) {
+                    v = (uint32_t)w;
+                    got = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            if (!got) {
+                // range rr has not published: its workgroup is not running
+                // yet (a GPU shared with other kernels dispatches each XCD's
+                // queue on its own, so an earlier workgroup can wait behind
+                // work that waits on this one).  Its counts are complete when
+                // this kernel starts: sum them here instead of waiting.
+                const uint32_t a0 = (uint32_t)((uint64_t)rr * nsp / G) << P.gshift;
+                const uint32_t a1 =
+                    min((uint32_t)((uint64_t)(rr + 1u) * nsp / G) << P.gshift, P.nchunk);
+                for (uint32_t c = a0; c < a1; ++c)
+                    v += P.cnt[(size_t)b * P.ncol + c];
+            }
+            if (v)
+                atomicAdd(&bs[b], v);
+        }
+        __syncthreads();
+        for (uint32_t e = t; e < nb * (crn + 1u); e += kLineBlock) {
+            const uint32_t b = e / (crn + 1u), j = e - b * (crn + 1u);
+            rt[b * P.rts + j] += bs[b];
+        }
+        __syncthreads();
+    }
     if (g0 >= g1)
         return;
-    if (!P.early) {
+    if (P.fused) {
+        pre0 = t < nb ? lsm[o.rt + t * P.rts] : 0u;
+        load_span(g0, pkA, qkA, 1u);
+    } else if (!P.early) {
         pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
         load_span(g0, pkA, qkA);
     }
@@ -1625,18 +1782,8 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         //   reads; a wave per bucket walked nb / 8 buckets in turn);
         // - the carried words into their stage slots;
         // - every packet at slot = tab[b][chunk] + rank.
-#ifdef YRSS_ABL_NOLOAD   // measurement builds only: no next-span stream loads
-        if (!last) {
-#pragma unroll
-            for (uint32_t k = 0; k < kG; ++k) {
-                pkn[k] = pk[k];
-                qkn[k] = qk[k];
-            }
-        }
-#else
         if (!last)
             load_span(g + 1u, pkn, qkn);
-#endif
         if (tj < tk) {
             const uint32_t b = opaque(tb);   // (addresses not hoisted: registers)
             // (bounded by the span's line count whatever the words say)
@@ -1734,9 +1881,6 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             if (mode == 0u) {
                 const uint32_t d = a0 - ph;
                 if (d + 4u <= P.n && d + 4u > d) {
-#ifdef YRSS_ABL_NOSTORE   // measurement builds only: the copy-out without its stores
-                    if (e.x == 0xffffffffu)
-#endif
                     if (P.nt)
                         list_store4<kListAuxMany>(lout, d, e);
                     else
@@ -2736,6 +2880,13 @@ struct yrss_ctx {
         uint32_t scan_epoch = 0;
         uint16_t *rank = nullptr;    // n x u16, grown on demand
         size_t rank_cap = 0;
+        // in-scatter prefixes: two totals sets (the parse kernel adds to set
+        // tot_set, its line scatter zeroes the other for the next batch) and
+        // the range aggregates' look-back words
+        uint32_t *tot_acc = nullptr;            // [2][nb]
+        uint32_t tot_set = 0;
+        unsigned long long *lb = nullptr;       // [kLbMaxWgs][kFusedMaxNb]
+        uint32_t lb_epoch = 0;
     };
     ListWs ws;
     uint32_t *d_fault_rec = nullptr;    // host-coherent fault record {code, kernel, where, value}
@@ -2840,6 +2991,7 @@ struct yrss_ctx {
         uint32_t line_groups = 0;     // force the line scatter's kG (2 or 4)
         uint32_t skip_line_check = 0; // launch a line scatter the host check refuses
         uint32_t partial_merge = 0;   // partial list lines as plain stores
+        int32_t lb_polls = -1;        // in-scatter prefixes' look-back polls (-1: kLbPolls)
     } dbg;
 };
 
@@ -3169,9 +3321,14 @@ int ensure_burst(yrss_ctx *c, uint32_t n)
 // hipHostRegister is process-wide, but each context keeps its own range table
 // (several contexts pipeline bursts over one mbuf pool), so registrations are
 // reference-counted per (base, len).
+// A range of a context closed after a GPU timeout is poisoned, not released:
+// a kernel that never finished may still read or write it, so it stays
+// registered for the life of the process, and registering that base again
+// fails (the application must not reuse the pool's address for a new one).
 struct HostReg {
     size_t len;
     uint32_t refs;
+    bool poisoned;
 };
 std::mutex g_reg_mu;
 std::map<void *, HostReg> g_reg;
@@ -3181,14 +3338,14 @@ hipError_t host_reg_acquire(void *base, size_t len)
     std::lock_guard<std::mutex> lk(g_reg_mu);
     auto it = g_reg.find(base);
     if (it != g_reg.end()) {
-        if (it->second.len != len)
+        if (it->second.len != len || it->second.poisoned)
             return hipErrorHostMemoryAlreadyRegistered;
         ++it->second.refs;
         return hipSuccess;
     }
     const hipError_t e = hipHostRegister(base, len, hipHostRegisterMapped);
     if (e == hipSuccess)
-        g_reg[base] = HostReg{len, 1u};
+        g_reg[base] = HostReg{len, 1u, false};
     return e;
 }
 
@@ -3196,12 +3353,25 @@ void host_reg_release(void *base)
 {
     std::lock_guard<std::mutex> lk(g_reg_mu);
     auto it = g_reg.find(base);
-    if (it == g_reg.end())
+    if (it == g_reg.end() || it->second.refs == 0)
         return;
-    if (--it->second.refs == 0) {
+    if (--it->second.refs == 0 && !it->second.poisoned) {
         (void)hipHostUnregister(base);
         g_reg.erase(it);
     }
+}
+
+// the hung-context path of yrss_fini: the context's reference is dropped,
+// the range stays registered and refuses new registrations
+void host_reg_poison(void *base)
+{
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.find(base);
+    if (it == g_reg.end())
+        return;
+    it->second.poisoned = true;
+    if (it->second.refs)
+        --it->second.refs;
 }
 
 int worker_halt(yrss_ctx *c);
@@ -3270,6 +3440,14 @@ hipError_t list_ws_alloc(yrss_ctx *c, yrss_ctx::ListWs &w)
         (e = hipMemset(w.scan_status, 0, st)) != hipSuccess ||
         (e = hipMemset(w.seg_cnt, 0, cnt)) != hipSuccess)
         return e;
+    if (c->nb <= kFusedMaxNb) {
+        const size_t lb = (size_t)kLbMaxWgs * kFusedMaxNb * sizeof(unsigned long long);
+        if ((e = hipMalloc((void **)&w.tot_acc, 2u * c->nb * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMemset(w.tot_acc, 0, 2u * c->nb * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMalloc((void **)&w.lb, lb)) != hipSuccess ||
+            (e = hipMemset(w.lb, 0, lb)) != hipSuccess)
+            return e;
+    }
     return hipSuccess;
 }
 
@@ -3279,6 +3457,8 @@ void list_ws_free(yrss_ctx::ListWs &w)
     (void)hipFree(w.seg_off);
     (void)hipFree(w.totals);
     (void)hipFree(w.scan_status);
+    (void)hipFree(w.tot_acc);
+    (void)hipFree(w.lb);
     (void)hipFree(w.rank);
     w = yrss_ctx::ListWs{};
 }
@@ -3637,6 +3817,8 @@ void yrss_fini(yrss_ctx *c)
             __atomic_store_n(&c->w.ctl->stop, 1u, __ATOMIC_RELEASE);
         fprintf(stderr, "yrss: context closed after a GPU timeout: not drained, device memory "
                         "left to process exit\n");
+        for (uint32_t r = 0; r < c->nranges; ++r)
+            host_reg_poison(c->range_base[r]);
         delete[] c->w.out;
         delete[] c->w.last_out;
         delete c;   // (shim_win stays: it may be registered for the GPU to read)
@@ -3794,6 +3976,35 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         YRSS_HIP(hipMalloc((void **)&W.rank, (size_t)n * sizeof(uint16_t)));
         W.rank_cap = n;
     }
+    // The line scatter's launch, planned before the parse kernel: with
+    // in-scatter prefixes (up to kFusedMaxNb buckets) the parse kernel sums
+    // the totals and no scan kernel runs.  Fused when the range table fits
+    // without costing the scatter a resident workgroup.
+    void (*line_fn)(LineParams) = nullptr;
+    uint32_t line_grid = 0, line_lds_bytes = lp.lds, rts = 0;
+    bool fused = false;
+    if (ranked) {
+        line_fn = lp.groups == 4u
+                      ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
+                      : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
+        // persistent: the resident workgroups, each one contiguous range of
+        // spans, never more workgroups than spans
+        const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
+        line_grid = std::max(1u, std::min(spans, resident_blocks(c, (const void *)line_fn,
+                                                                 kLineBlock, lp.lds)));
+        if (c->nb <= kFusedMaxNb && W.tot_acc && c->tune.scan_kernel == 0 &&
+            line_grid <= kLbMaxWgs) {
+            const uint32_t rc = ((spans + line_grid - 1) / line_grid) << lp.gshift;
+            const uint32_t lds = line_lds(c->nb, lp.gshift, lp.lmax, rc + 1u).words * 4u;
+            if ((uint64_t)c->nb * rc <= (uint64_t)kLineBlock * kFusedRegs && lds <= 160u * 1024u &&
+                std::min(spans, resident_blocks(c, (const void *)line_fn, kLineBlock, lds)) ==
+                    line_grid) {
+                fused = true;
+                rts = rc + 1u;
+                line_lds_bytes = lds;
+            }
+        }
+    }
     ParseParams P = c->proto;
     P.win = b->win;
     P.len = b->len;
@@ -3812,6 +4023,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     P.kni_bm = c->d_kni;
     P.kni_enable = c->kni_enable ? 1u : 0u;
     P.rank_pack = ranked && lp.packed ? 1u : 0u;
+    const uint32_t tset = W.tot_set;
+    P.tot_acc = fused ? W.tot_acc + (size_t)tset * c->nb : nullptr;
     {
         Timed t(c, YRSS_K_PARSE_HASH);
         hipExtLaunchKernelGGL(pick_parse(ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
@@ -3819,9 +4032,11 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
                               (uint32_t)parse_lds(filter), s, t.a, t.b, 0, P);
     }
     YRSS_HIP(hipGetLastError());
+    if (fused)
+        W.tot_set = tset ^ 1u;   // this batch's scatter zeroes it for the next
     if (!compact)
         return 0;
-    {
+    if (!fused) {
         Timed t(c, YRSS_K_SCAN);
         ScanParams SP;
         SP.cnt = W.seg_cnt;
@@ -3862,16 +4077,23 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         S.nt = c->nb > kListNtBuckets ? 1u : 0u;
         S.early = c->nb > 16u ? 1u : 0u;
         S.merge = c->dbg.partial_merge;
-        // persistent: the resident workgroups, each one contiguous range of
-        // spans, never more workgroups than spans
-        const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
-        void (*fn)(LineParams) =
-            lp.groups == 4u ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
-                            : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
-        const uint32_t sgrid =
-            std::min(spans, resident_blocks(c, (const void *)fn, kLineBlock, lp.lds));
+        S.fused = fused ? 1u : 0u;
+        S.cnt = W.seg_cnt;
+        S.lb = W.lb;
+        S.rts = rts;
+        S.tot_next = nullptr;
+        S.epoch = 0;
+        S.lb_polls = c->dbg.lb_polls < 0 ? kLbPolls : (uint32_t)c->dbg.lb_polls;
+        if (fused) {
+            S.totals = W.tot_acc + (size_t)tset * c->nb;
+            S.tot_next = W.tot_acc + (size_t)(tset ^ 1u) * c->nb;
+            S.xcd = 0;   // (ranges in blockIdx order: the kernel ignores it too)
+            if ((++W.lb_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
+                ++W.lb_epoch;
+            S.epoch = W.lb_epoch;
+        }
         Timed t(c, YRSS_K_SCATTER);
-        hipExtLaunchKernelGGL(fn, dim3(std::max(sgrid, 1u)), dim3(kLineBlock), lp.lds, s, t.a,
+        hipExtLaunchKernelGGL(line_fn, dim3(line_grid), dim3(kLineBlock), line_lds_bytes, s, t.a,
                               t.b, 0, S);
         YRSS_HIP(hipGetLastError());
         return 0;
@@ -3914,23 +4136,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
 
 extern "C" {
 
-#ifdef YRSS_PROF_LINES
-// measurement builds only: the line scatter's phase clock (tools/line_prof.py)
-int yrss_debug_line_prof(void *out, size_t bytes)
-{
-    // read, then clear (a later batch with fewer workgroups leaves no stale rows)
-    const size_t n = bytes < sizeof(g_line_prof) ? bytes : sizeof(g_line_prof);
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(out, HIP_SYMBOL(g_line_prof), n, 0, hipMemcpyDeviceToHost) !=
-            hipSuccess)
-        return -EIO;
-    static uint64_t zero[2048 * 8 * 8];
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_line_prof), zero, sizeof(zero), 0,
-                             hipMemcpyHostToDevice) == hipSuccess
-               ? (int)n
-               : -EIO;
-}
-#endif
+YRSS_LINE_PROF_HOST_FN   // (measurement builds only)
 
 int yrss_dispatch_dev(yrss_ctx *c, const uint8_t *d_win, uint32_t win_stride,
                       const uint16_t *d_len, uint32_t n, int16_t *d_q, uint32_t *d_hash,
@@ -4922,7 +5128,7 @@ int yrss_set_tuning(yrss_ctx *c, const struct yrss_tuning *t)
     const bool pow2 = (t->chunk_tiles & (t->chunk_tiles - 1u)) == 0 &&
                       (t->span_tiles & (t->span_tiles - 1u)) == 0;
     if (!pow2 || t->chunk_tiles > 4096u || t->span_tiles > 65536u || t->parse_blocks > 65536u ||
-        t->one_launch > 2u || t->scatter_xcd < -1 || t->scatter_xcd > 1)
+        t->one_launch > 2u || t->scatter_xcd < -1 || t->scatter_xcd > 1 || t->scan_kernel > 1u)
         return -EINVAL;
     if (c->pend.active)
         return -EBUSY;
@@ -4957,6 +5163,14 @@ int yrss_debug_partial_merge(yrss_ctx *c, int on)
     if (!c || on < 0 || on > 1)
         return -EINVAL;
     c->dbg.partial_merge = (uint32_t)on;
+    return 0;
+}
+
+int yrss_debug_lookback_polls(yrss_ctx *c, int polls)
+{
+    if (!c || polls < -1 || polls > 1000000)
+        return -EINVAL;
+    c->dbg.lb_polls = polls;
     return 0;
 }
 

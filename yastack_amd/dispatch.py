@@ -456,10 +456,10 @@ class SoftRss:
         return (int(f.code), int(f.kernel), int(f.where), int(f.value))
 
     def set_tuning(self, chunk_tiles: int = 0, span_tiles: int = 0, parse_blocks: int = 0,
-                   one_launch: int = 0, scatter_xcd: int = -1) -> None:
+                   one_launch: int = 0, scatter_xcd: int = -1, scan_kernel: int = 0) -> None:
         """Layout overrides for tests and measurements (yrss_set_tuning); the
         results never depend on them."""
-        t = abi.Tuning(chunk_tiles, span_tiles, parse_blocks, one_launch, scatter_xcd)
+        t = abi.Tuning(chunk_tiles, span_tiles, parse_blocks, one_launch, scatter_xcd, scan_kernel)
         abi.check(self._lib.yrss_set_tuning(self._ctx, ctypes.byref(t)), "yrss_set_tuning")
 
     def grid_for(self, n: int) -> int:
