@@ -671,6 +671,38 @@ def pcie_fanout(profile: str, world: int, place=None):
     return out or None
 
 
+def crossover_tcp_share(cpu, pcie):
+    """The hashed-TCP share of the traffic above which a host-resident GPU
+    form beats ONE reference dispatcher core end to end.  The CPU's time a
+    packet depends on the share s (the reference hashes TCP only,
+    ff_dpdk_if.c:1986-2058): 1 / R_cpu(s) = s / R_tcp + (1 - s) / R_udp, both
+    from cpu_baseline (bit-serial, through the dispatcher's function pointer,
+    1 core); the GPU's rate does not depend on s (it reads every window).  So
+    s* = (1 / R_gpu - 1 / R_udp) / (1 / R_tcp - 1 / R_udp), per worker row of
+    pcie_inclusive (median rate): 0 when the GPU form is faster even on all-UDP
+    traffic, null when it is slower even on all-TCP traffic."""
+    if not cpu or not pcie:
+        return None
+    try:
+        bp = cpu["by_profile"]
+        r_udp = float(bp["udp4"]["bit_serial_fnptr"]["1"]["mpps"])
+        r_tcp = float(bp["tcp4"]["bit_serial_fnptr"]["1"]["mpps"])
+    except (KeyError, TypeError, ValueError):
+        return None
+    rows = []
+    for row in pcie:
+        api = row.get("api", "")
+        if not api.startswith("yrss_worker") or not row.get("mpps"):
+            continue
+        r_gpu = float(row["mpps"])
+        s = (1.0 / r_gpu - 1.0 / r_udp) / (1.0 / r_tcp - 1.0 / r_udp)
+        rows.append({"api": api, "burst": row.get("burst"), "pool": row.get("pool"),
+                     "gpu_mpps": r_gpu,
+                     "tcp_share": None if s > 1.0 else round(max(s, 0.0), 4)})
+    return {"cpu_udp_mpps": r_udp, "cpu_tcp_mpps": r_tcp, "cores": 1,
+            "cpu_call": "bit-serial through the dispatcher's function pointer", "rows": rows}
+
+
 def load_traffic(path: str, key: dict, field: str = "hbm_bytes_per_launch"):
     """Per-launch HBM bytes (parse kernel, or `step_hbm_bytes` for the whole
     step) from a committed PMC summary of the same workload
@@ -1038,6 +1070,7 @@ def main(argv=None):
             "configs_extra": extra,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "pcie_inclusive_crossover_tcp_share": crossover_tcp_share(cpu, pcie),
             "pcie_fanout": fan,
             "check": check,
         }

@@ -36,12 +36,6 @@ int yrss_debug_line_groups(yrss_ctx *ctx, uint32_t groups, int skip_host_check);
  * 0: streaming stores like every other line (results unchanged). */
 int yrss_debug_partial_merge(yrss_ctx *ctx, int on);
 
-/* In-scatter list prefixes (up to 16 buckets): how often a line-scatter
- * workgroup polls an earlier range's published aggregate before summing that
- * range's chunk counts itself (the path a GPU shared with other kernels
- * takes); -1 = the built-in count, 0 = always sum (results unchanged). */
-int yrss_debug_lookback_polls(yrss_ctx *ctx, int polls);
-
 #ifdef __cplusplus
 }
 #endif

@@ -31,8 +31,8 @@ def test_shipping_library_has_no_test_or_measurement_paths():
     libyrss_test.so only, the phase clock (YRSS_PROF_LINES) only in
     tools/build_ab_lib.sh builds, and no hook reads the environment."""
     hooks = abi.header_functions(abi.REPO_DIR / "include" / "yrss_test_hooks.h")
-    assert hooks == ["yrss_debug_line_groups", "yrss_debug_lookback_polls",
-                     "yrss_debug_partial_merge", "yrss_debug_worker_inject"]
+    assert hooks == ["yrss_debug_line_groups", "yrss_debug_partial_merge",
+                     "yrss_debug_worker_inject"]
     ship = subprocess.run(["nm", "-D", "--defined-only", str(abi.LIB_PATH)],
                           capture_output=True, text=True, check=True).stdout
     assert not re.findall(r"\bT (yrss_debug_\w+)", ship)

@@ -289,19 +289,3 @@ def test_in_scatter_prefixes(dev, oracle_mod, cfg):
             eng.set_tuning(chunk_tiles=chunk, span_tiles=span)
             check(eng, oracle_mod, cfg, abi.SYN_FUZZ, (1 << 21) + 3, first=13)
 
-
-@pytest.mark.parametrize("polls", [0, 1])
-@pytest.mark.parametrize("cfg", [(3, 3, 1, 1), (15, 15, 1, 0)])
-def test_in_scatter_prefixes_without_lookback(dev, oracle_mod, cfg, polls):
-    """A line-scatter workgroup that does not see an earlier range's aggregate
-    within its polls sums that range's chunk counts itself (the path of a GPU
-    shared with other kernels, where an earlier workgroup may not be running
-    yet): forced through libyrss_test.so's hook, every range or most of them
-    take it, and the lists are the same."""
-    with SoftRss(*cfg, device=0, max_burst=0, lib_path=str(abi.TEST_LIB_PATH)) as eng:
-        assert eng._lib.yrss_debug_lookback_polls(eng._ctx, polls) == 0
-        for k, n in enumerate((77777, (1 << 22) + 77, 1 << 24)):
-            check(eng, oracle_mod, cfg, (abi.SYN_TCP4, abi.SYN_FUZZ, abi.SYN_IMIX)[k], n,
-                  first=k * 31)
-        assert eng._lib.yrss_debug_lookback_polls(eng._ctx, -1) == 0
-        check(eng, oracle_mod, cfg, abi.SYN_IMIX, 1 << 20, first=5)

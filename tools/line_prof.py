@@ -34,6 +34,8 @@ def main() -> int:
     ap.add_argument("--groups", type=int, default=0,
                     help="force the line-scatter kernel (yrss_debug_line_groups: 2 / 4 kG); "
                          "needs a -DYRSS_TEST_HOOKS build")
+    ap.add_argument("--scan-kernel", type=int, default=0,
+                    help="1: list prefixes from the scan kernel (yrss_tuning.scan_kernel)")
     args = ap.parse_args()
     lib = abi.load(str(ROOT / args.lib))
     lib.yrss_debug_line_prof.restype = ctypes.c_int
@@ -43,6 +45,8 @@ def main() -> int:
         e = SoftRss(npr, npr, 1, 1, device=0, max_burst=0, lib_path=str(ROOT / args.lib))
         if args.groups:
             assert e._lib.yrss_debug_line_groups(e._ctx, args.groups, 0) == 0
+        if args.scan_kernel:
+            e.set_tuning(scan_kernel=1)
         w, l = e.synth(abi.SYN_TCP4, n, 0)
         out = e.alloc_out(n, w.device)
         buf = np.zeros(2048 * 8 * 8, np.uint64)
@@ -63,7 +67,7 @@ def main() -> int:
             print(f"q{npr}: no spans (one-list batch)")
             e.close()
             continue
-        print(f"q{npr} groups {args.groups}: {blocks} workgroups, spans per workgroup {spans.min()}-{spans.max()}")
+        print(f"q{npr} groups {args.groups} scan_kernel {args.scan_kernel}: {blocks} workgroups, spans per workgroup {spans.min()}-{spans.max()}")
         for k, name in enumerate(PH):
             v = d[:, :, k][m[:, :, k]]
             if v.size == 0:
@@ -92,6 +96,20 @@ def main() -> int:
                   f"{pro.mean():.0f} p90 {np.percentile(pro, 90):.0f} ns")
             if lbend.size and (lbend > 0).all():
                 print(f"   entry -> look-back done mean {((lbend - entry) * 10).mean():.0f} ns")
+            # prologue milestones (slots 1-5 of the span-7 row): totals scanned,
+            # one-list barrier passed, in-scatter prefixes done, first layout
+            # barrier passed, first span's streams arrived
+            pro_ms = p[:, 7, 1:6][used[:, 0]]
+            names = ["totals scanned", "one-list barrier", "range prefixes", "first layout",
+                     "streams arrived"]
+            prev = entry
+            for k, nm in enumerate(names):
+                col = pro_ms[:, k]
+                ok = col > 0
+                if ok.any():
+                    print(f"   prologue: -> {nm:18s} mean {((col - prev)[ok] * 10).mean():7.0f} ns")
+                    prev = np.where(ok, col, prev)
+            print(f"   prologue: -> first span         mean {((first - prev) * 10).mean():7.0f} ns")
             endk = (ends - k0) * 10
             ids = np.nonzero(used[:, 0])[0]
             print(f"   end after first entry: p10 {np.percentile(endk, 10):.0f} p50 "

@@ -242,7 +242,6 @@ _TEST_PROTOS = {
     "yrss_debug_worker_inject": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "yrss_debug_line_groups": (ctypes.c_int, [_vp, _u32, ctypes.c_int]),
     "yrss_debug_partial_merge": (ctypes.c_int, [_vp, ctypes.c_int]),
-    "yrss_debug_lookback_polls": (ctypes.c_int, [_vp, ctypes.c_int]),
 }
 
 _lib = None

@@ -55,6 +55,7 @@ constexpr int kTile = 64;              // packets per wave-tile (one per lane)
 constexpr int kScatterBlock = 256;     // 4 waves per scatter workgroup (halved for large nb)
 constexpr int kScatterWaves = kScatterBlock / kWave;
 constexpr uint32_t kMaxChunks = 65536;  // per launch; bounds the count matrix [nb][ncol]
+constexpr uint32_t kLbMaxWgs = 2048;    // line-scatter ranges a range-bin row holds
 constexpr uint32_t kCntWords = 2176;    // parse: per-wave LDS count slots (chunks x nb): 32 x 68
 // scan: chunk columns per workgroup are up to kScanSub sub-tiles of 4096
 // (ScanParams.sub): two where the columns come in whole 8192s, so a 65-bucket
@@ -105,6 +106,8 @@ struct ParseParams {
     uint32_t rank_pack;   // kCount == 2: the rank word is bucket << (ct_shift + 6) | rank
     uint32_t *tot_acc;    // kCount: per-bucket totals, added to (zeroed by the previous
                           // line scatter), or null (the scan kernel sums them)
+    uint32_t *rbin;       // with tot_acc: [nb][kLbMaxWgs] counts per line-scatter range
+    uint32_t rbin_chunks; // chunks a range (a multiple of 8)
     uint32_t kwin[96];    // key window at every tuple bit position
 };
 
@@ -684,10 +687,14 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
         // With tot_acc the workgroup also sums its counts per bucket (in the
         // staging LDS, free after the loop) and adds them to the batch totals,
         // so the line scatter needs no scan kernel in front of it
+        // and, per round j, the 8 waves' counts of each bucket (their 8
+        // consecutive columns g0 + j W + w lie in one scatter range: ranges
+        // are multiples of 8 chunks and g0 of 8), added to that range's bin
         uint32_t *wtot = reinterpret_cast<uint32_t *>(smem + kTblBytes);
+        uint32_t *jtot = wtot + P.nb;   // [kmax][nb] (kmax nb <= kCntWords)
         const bool tot = P.tot_acc != nullptr;   // (uniform)
         if (tot) {
-            for (uint32_t e = threadIdx.x; e < P.nb; e += kBlock)
+            for (uint32_t e = threadIdx.x; e < P.nb * (kmax + 1u); e += kBlock)
                 wtot[e] = 0u;
             __syncthreads();
         }
@@ -702,8 +709,10 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
             if (col < P.nchunk && (j + 1u) * P.nb <= kCntWords) {
                 const uint32_t v = cnt_base[w * kCntWords + j * P.nb + b];
                 P.seg_cnt[(size_t)b * P.ncol + col] = v;
-                if (tot && v)
+                if (tot && v) {
                     atomicAdd(&wtot[b], v);
+                    atomicAdd(&jtot[j * P.nb + b], v);
+                }
             }
             b += kBlock / kWaves;
             while (b >= P.nb) {
@@ -717,6 +726,12 @@ __global__ __launch_bounds__(kBlock) void yrss_parse_hash(ParseParams P)
                 if (wtot[e])
                     __hip_atomic_fetch_add(P.tot_acc + e, wtot[e], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t e = threadIdx.x; e < kmax * P.nb; e += kBlock) {
+                const uint32_t jj = e / P.nb, bb = e - jj * P.nb;
+                if (jtot[e])
+                    __hip_atomic_fetch_add(P.rbin + bb * kLbMaxWgs + (g0 + jj * W) / P.rbin_chunks,
+                                           jtot[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
 }
@@ -1249,15 +1264,13 @@ constexpr uint32_t line_span_max(uint32_t g) { return kLineBlock * 8u * g; }
 constexpr uint32_t line_bucket_regs(uint32_t g) { return g == 2u ? 2u : 8u; }
 constexpr uint32_t line_nb_max(uint32_t g) { return 64u * line_bucket_regs(g); }
 // In-scatter prefixes (LineParams.fused) up to 16 buckets: the scan kernel and
-// its launch gap leave the step.  A range's nb x chunks counts are loaded in
-// kFusedRegs registers a thread; the look-back words are sized for
-// kLbMaxWgs workgroups.
+// its launch gap leave the step.  Waves 1-7 of a workgroup take a bucket row
+// each (up to kFusedRows): its counts over the range's chunks and its bins of
+// the earlier ranges; the range bins are [nb][kLbMaxWgs].
 constexpr uint32_t kFusedMaxNb = 16;
-constexpr uint32_t kFusedRegs = 6;
-constexpr uint32_t kLbMaxWgs = 2048;
-// polls of an earlier range's aggregate (a round trip each, ~1 us) before the
-// workgroup sums that range's counts itself
-constexpr uint32_t kLbPolls = 24;
+constexpr uint32_t kFusedRows = 3;          // bucket rows a loading wave (waves 1-7)
+constexpr uint32_t kFusedMaxCols = 256;      // chunks a range: 4 a lane
+constexpr uint32_t kFusedMaxRanges = 512;    // earlier ranges' bins: 8 a lane
 static_assert(line_nb_max(4) <= (uint32_t)kLineBlock, "tagging: a thread to a bucket at least");
 
 
@@ -1278,21 +1291,23 @@ struct LineParams {
     uint32_t early;            // first span's loads before the totals: past 16 buckets
     uint32_t merge;            // partial lines (a range's first / last) as plain stores: L2 merges
     // In-scatter prefixes (fused, up to kFusedMaxNb buckets): no scan kernel
-    // runs; totals are the parse kernel's sums, each workgroup scans its own
-    // range's chunk counts in LDS and adds the aggregates of the earlier ranges
+    // runs.  The parse kernel sums the totals and, per scatter range of rcs
+    // spans, the range's counts (range bins); each workgroup scans its own
+    // range's chunk counts in LDS from the sum of the earlier ranges' bins.
     const uint32_t *cnt;       // [nb][ncol] per-chunk counts (the parse kernel's)
-    uint32_t *tot_next;        // the totals set the next batch's parse kernel adds to: zeroed
-    unsigned long long *lb;    // [grid][nb] range aggregates: flag | epoch:31 | value:32
-    uint32_t fused, epoch;
+    const uint32_t *rbin;      // [nb][kLbMaxWgs] range bins (the parse kernel's)
+    uint32_t *tot_next;        // the next batch's totals set: zeroed here
+    uint32_t *rbin_next;       // the next batch's range bins: zeroed here
+    uint32_t fused;
+    uint32_t rcs;              // spans a range
     uint32_t rts;              // row stride of the range table: range chunks + 1
-    uint32_t lb_polls;         // polls of an earlier range's aggregate (kLbPolls)
 };
 
 // LDS of a workgroup, in words: per-bucket arrays, the prefix table, the
 // carried lines, the stage's line tags, the stage (+ a spare word); with
-// in-scatter prefixes also the range table and the range bases.
+// in-scatter prefixes also the range table.
 struct LineLds {
-    uint32_t start, cs, ve, ce, so, rb, lsl, misc, tab, cb, ltag, lgl, stg, rt, bs, words;
+    uint32_t start, cs, ve, ce, so, rb, lsl, misc, tab, cb, ltag, lgl, stg, rt, words;
 };
 __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32_t lmax,
                                             uint32_t rts = 0)
@@ -1319,7 +1334,6 @@ __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32
     L.lgl = take(lmax);   // the line's list line (adjusted position / 16)
     L.stg = take(16u * lmax + 4u);
     L.rt = take(nb * rts);   // [nb][rts]: the range's chunk prefixes, then its end
-    L.bs = take(rts ? nb : 0u);
     L.words = o;
     return L;
 }
@@ -1387,13 +1401,20 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
 
     // this workgroup's range of spans
     const uint32_t nsp = (uint32_t)(((uint64_t)P.n + P.seg - 1u) / P.seg);
-    // (in-scatter prefixes wait on the ranges before their own: ranges in
-    // blockIdx order, so those were dispatched first)
+    // (in-scatter prefixes: ranges of rcs spans in blockIdx order, the
+    // partition the parse kernel's range bins were summed by)
     const uint32_t r = P.fused ? blockIdx.x : xcd_block(P.xcd), G = gridDim.x;
-    if (P.fused && blockIdx.x == 0 && t < nb)
-        P.tot_next[t] = 0u;   // read by no one in this kernel
-    const uint32_t g0 = (uint32_t)((uint64_t)r * nsp / G);
-    const uint32_t g1 = (uint32_t)((uint64_t)(r + 1u) * nsp / G);
+    const uint32_t g0 = P.fused ? min(r * P.rcs, nsp) : (uint32_t)((uint64_t)r * nsp / G);
+    const uint32_t g1 = P.fused ? min(g0 + P.rcs, nsp) : (uint32_t)((uint64_t)(r + 1u) * nsp / G);
+    if (P.fused) {
+        // the next batch's totals and range bins start from zero (no one
+        // reads them in this kernel; each workgroup clears a slice)
+        if (blockIdx.x == 0 && t < nb)
+            P.tot_next[t] = 0u;
+        const uint32_t zw = kLbMaxWgs * nb, per = (zw + G - 1u) / G;
+        for (uint32_t e = r * per + t; e < min(zw, (r + 1u) * per); e += kLineBlock)
+            P.rbin_next[e] = 0u;
+    }
     // prefix table rows are ncs + 1 words apart: with a power-of-two row the
     // lanes of one chunk column hit one or two LDS banks whatever their bucket
     // (a 0.78 conflict share of the LDS cycles at 64 buckets)
@@ -1511,35 +1532,16 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // them must not wait for the first span's streams behind them.
     constexpr uint32_t kTB = line_bucket_regs(kG);   // nb <= 64 kTB (checked at entry)
     uint32_t tv[kTB];
-    if (wave == 0) {
+    auto load_totals = [&]() {   // (wave 0)
+        const __amdgpu_buffer_rsrc_t rt_ = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(P.totals), 0, (int)(nb * 4u), kRsrcWord3);
 #pragma unroll
-        for (uint32_t i = 0; i < kTB; ++i) {
-            const uint32_t b = i * kWave + lane;
-            tv[i] = i * kWave < nb && b < nb ? P.totals[b] : 0u;
-        }
-    }
-    // in-scatter prefixes: the range's chunk counts are loaded beside the
-    // totals (one round trip for both; after them, so waiting for the totals
-    // does not wait for these), element i 512 + t of the range's nb x crn
-    // counts a thread (the host keeps nb x crn <= 512 kFusedRegs)
-    uint32_t cv[kFusedRegs];
-    if (P.fused) {
-        const uint32_t cr0 = g0 << P.gshift;
-        crn = g0 < g1 ? min(g1 << P.gshift, P.nchunk) - cr0 : 0u;
-#pragma unroll
-        for (uint32_t i = 0; i < kFusedRegs; ++i) {
-            const uint32_t e = i * kLineBlock + t, b = crn ? e / crn : 0u;
-            cv[i] = b < nb ? P.cnt[(size_t)b * P.ncol + cr0 + (e - b * crn)] : 0u;
-        }
-    }
-    // Past 16 buckets the first span's prefixes and streams are issued before
-    // the totals are scanned, so the round trips overlap (such batches are
-    // rarely one-list, where these loads go unused)
-    if (P.early && g0 < g1) {
-        pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
-        load_span(g0, pkA, qkA);
-    }
-    if (wave == 0) {
+        for (uint32_t i = 0; i < kTB; ++i)
+            tv[i] = i * kWave < nb ? __builtin_amdgcn_raw_buffer_load_b32(
+                                         rt_, (int)((i * kWave + lane) * 4u), 0, 0)
+                                   : 0u;
+    };
+    auto scan_totals = [&]() {   // (wave 0)
         uint32_t carry = 0, nzb = 0;
 #pragma unroll
         for (uint32_t i = 0; i < kTB; ++i) {
@@ -1563,8 +1565,64 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             misc[1] = 0u;
             misc[3] = 0u;
         }
+        LPROF_PRO(1);
+    };
+    // In-scatter prefixes: waves 1-7 take the bucket rows b = wave - 1,
+    // wave + 6, ... (nb <= 16: three at most) and load, a lane 16 bytes at a
+    // time, the row's counts over the range's chunks (crn <= 256 columns) and
+    // its bins of every earlier range (r <= 512), while wave 0 loads and
+    // scans the totals.  Nine 16-byte loads a lane at most, no divisions:
+    // the waves reach the one-list barrier at once, and wave 0 waits for the
+    // totals alone (its loads and their use sit in one branch: split in two,
+    // the compiler waited for every load of the other waves' path at the
+    // barrier), so the one-list path is not held up by these loads.
+    constexpr uint32_t kFR = kFusedRows;
+    u32x4 fc[kFR], fb0[kFR], fb1[kFR];
+    if (P.fused) {
+        const uint32_t cr0 = g0 << P.gshift;
+        crn = g0 < g1 ? min(g1 << P.gshift, P.nchunk) - cr0 : 0u;
+    }
+    if (P.early) {
+        // Past 16 buckets the first span's prefixes and streams are issued
+        // after the totals and before they are scanned, so the round trips
+        // overlap (such batches are rarely one-list, where these loads go
+        // unused)
+        if (wave == 0)
+            load_totals();
+        if (g0 < g1) {
+            pre0 = t < nb ? prefix(t, g0 << P.gshift) : 0u;
+            load_span(g0, pkA, qkA);
+        }
+        if (wave == 0)
+            scan_totals();
+    } else if (wave == 0) {
+        load_totals();
+        scan_totals();
+    } else if (P.fused) {
+        const uint32_t cr0 = g0 << P.gshift;
+        const __amdgpu_buffer_rsrc_t rc_ = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(P.cnt), 0, (int)(nb * P.ncol * 4u), kRsrcWord3);
+        const __amdgpu_buffer_rsrc_t rb_ = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(P.rbin), 0, (int)(nb * kLbMaxWgs * 4u), kRsrcWord3);
+#pragma unroll
+        for (uint32_t k = 0; k < kFR; ++k) {
+            const uint32_t b = wave - 1u + k * (kLineBlock / kWave - 1u);
+            const uint32_t bo = b < nb ? b : nb;   // rows past nb: past the range, read 0
+            // (lanes past the range's columns or the earlier ranges read past
+            // the buffer: the range check returns 0 and nothing is fetched,
+            // which a one-list batch, where these go unused, would pay for)
+            constexpr uint32_t kOut = 0x7ffffff0u;
+            fc[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rc_, (int)(4u * lane < crn ? (bo * P.ncol + cr0 + 4u * lane) * 4u : kOut), 0, 0));
+            fb0[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rb_, (int)(8u * lane < r ? (bo * kLbMaxWgs + 8u * lane) * 4u : kOut), 0, 0));
+            fb1[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rb_, (int)(8u * lane + 4u < r ? (bo * kLbMaxWgs + 8u * lane + 4u) * 4u : kOut),
+                0, 0));
+        }
     }
     __syncthreads();
+    LPROF_PRO(2);
     if (misc[0] == 1u) {
         // one non-empty list (all-UDP traffic): 0, 1, ..., n-1, grid-stride
         // 16-byte non-temporal stores (64 MB in 10.7 us,
@@ -1588,80 +1646,54 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     }
 
     if (P.fused) {
-        // In-scatter prefixes.  (1) The range's chunk counts into the range
-        // table, then per bucket an exclusive scan over them (a wave to a
-        // row), the row's total at column crn; the totals are published as
-        // this range's aggregates at once.  (2) The range's base per bucket:
-        // the aggregates of every earlier range, read at once (a pair a
-        // thread; ranges in blockIdx order, so on an unshared GPU every range
-        // waited for was dispatched earlier).
-        // (3) base added to every column.  Every span's prefixes then come
-        // from LDS.  No workgroup waits without bound: an aggregate that does
-        // not appear within lb_polls polls is summed from the counts instead.
-        uint32_t *rt = lsm + o.rt, *bs = lsm + o.bs;
-        // the first span's streams ride under the range scan and the look-back
+        // In-scatter prefixes, from what the parse kernel left (all of it
+        // complete when this kernel starts, so no workgroup waits on another):
+        // the range's chunk counts go into the range table, the earlier
+        // ranges' bins add up to the range's base per bucket, and a wave to a
+        // bucket row scans the row starting from that base; column crn gets
+        // the range's end.  Every span's prefixes then come from LDS.
+        uint32_t *rt = lsm + o.rt;
+        if (wave != 0) {
+            // a row: the bins of the ranges before this one (words past r
+            // masked) add up to the row's base; the counts (words past crn
+            // masked), scanned across the wave from that base, are the row's
+            // exclusive prefixes; column crn gets the range's end
+#pragma unroll
+            for (uint32_t k = 0; k < kFR; ++k) {
+                const uint32_t b = wave - 1u + k * (kLineBlock / kWave - 1u);
+                if (b >= nb)   // (uniform)
+                    break;
+                const uint32_t q0 = 8u * lane;
+                const uint32_t bins = (q0 + 0u < r ? fb0[k].x : 0u) + (q0 + 1u < r ? fb0[k].y : 0u) +
+                                      (q0 + 2u < r ? fb0[k].z : 0u) + (q0 + 3u < r ? fb0[k].w : 0u) +
+                                      (q0 + 4u < r ? fb1[k].x : 0u) + (q0 + 5u < r ? fb1[k].y : 0u) +
+                                      (q0 + 6u < r ? fb1[k].z : 0u) + (q0 + 7u < r ? fb1[k].w : 0u);
+                const uint32_t base = __shfl(wave_incl_scan(bins, lane), kWave - 1, kWave);
+                const uint32_t c0 = 4u * lane;
+                const uint32_t x0 = c0 + 0u < crn ? fc[k].x : 0u, x1 = c0 + 1u < crn ? fc[k].y : 0u;
+                const uint32_t x2 = c0 + 2u < crn ? fc[k].z : 0u, x3 = c0 + 3u < crn ? fc[k].w : 0u;
+                const uint32_t sum = x0 + x1 + x2 + x3;
+                const uint32_t inc = wave_incl_scan(sum, lane);
+                const uint32_t tot = __shfl(inc, kWave - 1, kWave);   // (every lane: a shuffle)
+                uint32_t *row = rt + b * P.rts;
+                uint32_t run = base + inc - sum;
+                if (c0 + 0u < crn) row[c0 + 0u] = run;
+                run += x0;
+                if (c0 + 1u < crn) row[c0 + 1u] = run;
+                run += x1;
+                if (c0 + 2u < crn) row[c0 + 2u] = run;
+                run += x2;
+                if (c0 + 3u < crn) row[c0 + 3u] = run;
+                if (lane == 0)
+                    row[crn] = base + tot;
+            }
+        }
+        // the first span's streams, after the rows (whose loads are then
+        // waited for alone), in flight under the first layout
         if (g0 < g1)
             load_span(g0, pkA, qkA, 2u);
-#pragma unroll
-        for (uint32_t i = 0; i < kFusedRegs; ++i) {
-            const uint32_t e = i * kLineBlock + t, b = crn ? e / crn : 0u;
-            if (b < nb)
-                rt[b * P.rts + (e - b * crn)] = cv[i];
-        }
-        if (t < nb)
-            bs[t] = 0u;
         __syncthreads();
-        for (uint32_t b = wave; b < nb; b += kLineBlock / kWave) {
-            uint32_t carry = 0;
-            for (uint32_t j0 = 0; j0 < crn; j0 += kWave) {
-                const uint32_t j = j0 + lane;
-                const uint32_t x = j < crn ? rt[b * P.rts + j] : 0u;
-                const uint32_t s = wave_incl_scan(x, lane);
-                if (j < crn)
-                    rt[b * P.rts + j] = carry + s - x;
-                carry += __shfl(s, kWave - 1, kWave);
-            }
-            if (lane == 0) {
-                rt[b * P.rts + crn] = carry;
-                __hip_atomic_store(P.lb + (size_t)r * nb + b, scan_status(P.epoch, false, carry),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        for (uint32_t e = t; e < r * nb; e += kLineBlock) {
-            const uint32_t rr = e / nb, b = e - rr * nb;
-            uint32_t v = 0;
-            bool got = false;
-            for (uint32_t polls = 0; polls < P.lb_polls; ++polls) {
-                const unsigned long long w =
-                    __hip_atomic_load(P.lb + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)((w >> 32) & 0x7fffffffu) == (P.epoch & 0x7fffffffu)) {
-                    v = (uint32_t)w;
-                    got = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
-            }
-            if (!got) {
-                // range rr has not published: its workgroup is not running
-                // yet (a GPU shared with other kernels dispatches each XCD's
-                // queue on its own, so an earlier workgroup can wait behind
-                // work that waits on this one).  Its counts are complete when
-                // this kernel starts: sum them here instead of waiting.
-                const uint32_t a0 = (uint32_t)((uint64_t)rr * nsp / G) << P.gshift;
-                const uint32_t a1 =
-                    min((uint32_t)((uint64_t)(rr + 1u) * nsp / G) << P.gshift, P.nchunk);
-                for (uint32_t c = a0; c < a1; ++c)
-                    v += P.cnt[(size_t)b * P.ncol + c];
-            }
-            if (v)
-                atomicAdd(&bs[b], v);
-        }
-        __syncthreads();
-        for (uint32_t e = t; e < nb * (crn + 1u); e += kLineBlock) {
-            const uint32_t b = e / (crn + 1u), j = e - b * (crn + 1u);
-            rt[b * P.rts + j] += bs[b];
-        }
-        __syncthreads();
+        LPROF_PRO(3);
     }
     if (g0 >= g1)
         return;
@@ -1749,11 +1781,13 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     if (wave == 0)
         layout(g0, 0u);
     __syncthreads();
+    LPROF_PRO(4);
     write_tab(0u);
     // nothing pending at the loop head: a pending load there made the
     // compiler wait vmcnt(0) at a first use in every span, i.e. for the
     // previous span's list stores as well
     __builtin_amdgcn_s_waitcnt(kWaitVm0);
+    LPROF_PRO(5);
     __syncthreads();
     // words written and their sum: a range is complete iff it wrote each of
     // its packets once, so the sum must be that of its packet indices (two
@@ -2880,13 +2914,12 @@ struct yrss_ctx {
         uint32_t scan_epoch = 0;
         uint16_t *rank = nullptr;    // n x u16, grown on demand
         size_t rank_cap = 0;
-        // in-scatter prefixes: two totals sets (the parse kernel adds to set
-        // tot_set, its line scatter zeroes the other for the next batch) and
-        // the range aggregates' look-back words
+        // in-scatter prefixes: two sets of totals and range bins (the parse
+        // kernel adds to set tot_set, its line scatter zeroes the other for
+        // the next batch)
         uint32_t *tot_acc = nullptr;            // [2][nb]
         uint32_t tot_set = 0;
-        unsigned long long *lb = nullptr;       // [kLbMaxWgs][kFusedMaxNb]
-        uint32_t lb_epoch = 0;
+        uint32_t *rbin = nullptr;               // [2][kLbMaxWgs][nb]
     };
     ListWs ws;
     uint32_t *d_fault_rec = nullptr;    // host-coherent fault record {code, kernel, where, value}
@@ -2991,7 +3024,6 @@ struct yrss_ctx {
         uint32_t line_groups = 0;     // force the line scatter's kG (2 or 4)
         uint32_t skip_line_check = 0; // launch a line scatter the host check refuses
         uint32_t partial_merge = 0;   // partial list lines as plain stores
-        int32_t lb_polls = -1;        // in-scatter prefixes' look-back polls (-1: kLbPolls)
     } dbg;
 };
 
@@ -3441,11 +3473,11 @@ hipError_t list_ws_alloc(yrss_ctx *c, yrss_ctx::ListWs &w)
         (e = hipMemset(w.seg_cnt, 0, cnt)) != hipSuccess)
         return e;
     if (c->nb <= kFusedMaxNb) {
-        const size_t lb = (size_t)kLbMaxWgs * kFusedMaxNb * sizeof(unsigned long long);
+        const size_t rb = 2u * kLbMaxWgs * c->nb * sizeof(uint32_t);
         if ((e = hipMalloc((void **)&w.tot_acc, 2u * c->nb * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMemset(w.tot_acc, 0, 2u * c->nb * sizeof(uint32_t))) != hipSuccess ||
-            (e = hipMalloc((void **)&w.lb, lb)) != hipSuccess ||
-            (e = hipMemset(w.lb, 0, lb)) != hipSuccess)
+            (e = hipMalloc((void **)&w.rbin, rb)) != hipSuccess ||
+            (e = hipMemset(w.rbin, 0, rb)) != hipSuccess)
             return e;
     }
     return hipSuccess;
@@ -3458,7 +3490,7 @@ void list_ws_free(yrss_ctx::ListWs &w)
     (void)hipFree(w.totals);
     (void)hipFree(w.scan_status);
     (void)hipFree(w.tot_acc);
-    (void)hipFree(w.lb);
+    (void)hipFree(w.rbin);
     (void)hipFree(w.rank);
     w = yrss_ctx::ListWs{};
 }
@@ -3981,7 +4013,7 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     // the totals and no scan kernel runs.  Fused when the range table fits
     // without costing the scatter a resident workgroup.
     void (*line_fn)(LineParams) = nullptr;
-    uint32_t line_grid = 0, line_lds_bytes = lp.lds, rts = 0;
+    uint32_t line_grid = 0, line_lds_bytes = lp.lds, rts = 0, rcs = 0;
     bool fused = false;
     if (ranked) {
         line_fn = lp.groups == 4u
@@ -3992,15 +4024,19 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
         line_grid = std::max(1u, std::min(spans, resident_blocks(c, (const void *)line_fn,
                                                                  kLineBlock, lp.lds)));
-        if (c->nb <= kFusedMaxNb && W.tot_acc && c->tune.scan_kernel == 0 &&
-            line_grid <= kLbMaxWgs) {
-            const uint32_t rc = ((spans + line_grid - 1) / line_grid) << lp.gshift;
+        if (c->nb <= kFusedMaxNb && W.tot_acc && c->tune.scan_kernel == 0) {
+            // ranges of rcs spans (the last ones may be shorter), rc chunks
+            const uint32_t rcs_ = (spans + line_grid - 1) / line_grid;
+            const uint32_t g_eff = (spans + rcs_ - 1) / rcs_;
+            const uint32_t rc = rcs_ << lp.gshift;
             const uint32_t lds = line_lds(c->nb, lp.gshift, lp.lmax, rc + 1u).words * 4u;
-            if ((uint64_t)c->nb * rc <= (uint64_t)kLineBlock * kFusedRegs && lds <= 160u * 1024u &&
-                std::min(spans, resident_blocks(c, (const void *)line_fn, kLineBlock, lds)) ==
-                    line_grid) {
+            if (rc % 8u == 0 && rc <= kFusedMaxCols && g_eff <= kFusedMaxRanges &&
+                c->nb <= kFusedRows * (kLineBlock / kWave - 1u) && lds <= 160u * 1024u &&
+                resident_blocks(c, (const void *)line_fn, kLineBlock, lds) >= g_eff) {
                 fused = true;
+                rcs = rcs_;
                 rts = rc + 1u;
+                line_grid = g_eff;
                 line_lds_bytes = lds;
             }
         }
@@ -4025,6 +4061,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     P.rank_pack = ranked && lp.packed ? 1u : 0u;
     const uint32_t tset = W.tot_set;
     P.tot_acc = fused ? W.tot_acc + (size_t)tset * c->nb : nullptr;
+    P.rbin = fused ? W.rbin + (size_t)tset * kLbMaxWgs * c->nb : nullptr;
+    P.rbin_chunks = fused ? rcs << lp.gshift : 0u;
     {
         Timed t(c, YRSS_K_PARSE_HASH);
         hipExtLaunchKernelGGL(pick_parse(ranked ? 2 : compact ? 1 : 0, filter), dim3(grid),
@@ -4079,18 +4117,17 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
         S.merge = c->dbg.partial_merge;
         S.fused = fused ? 1u : 0u;
         S.cnt = W.seg_cnt;
-        S.lb = W.lb;
+        S.rbin = nullptr;
+        S.rbin_next = nullptr;
         S.rts = rts;
+        S.rcs = rcs;
         S.tot_next = nullptr;
-        S.epoch = 0;
-        S.lb_polls = c->dbg.lb_polls < 0 ? kLbPolls : (uint32_t)c->dbg.lb_polls;
         if (fused) {
             S.totals = W.tot_acc + (size_t)tset * c->nb;
             S.tot_next = W.tot_acc + (size_t)(tset ^ 1u) * c->nb;
+            S.rbin = W.rbin + (size_t)tset * kLbMaxWgs * c->nb;
+            S.rbin_next = W.rbin + (size_t)(tset ^ 1u) * kLbMaxWgs * c->nb;
             S.xcd = 0;   // (ranges in blockIdx order: the kernel ignores it too)
-            if ((++W.lb_epoch & 0x7fffffffu) == 0)   // 0 is the never-published state
-                ++W.lb_epoch;
-            S.epoch = W.lb_epoch;
         }
         Timed t(c, YRSS_K_SCATTER);
         hipExtLaunchKernelGGL(line_fn, dim3(line_grid), dim3(kLineBlock), line_lds_bytes, s, t.a,
@@ -5163,14 +5200,6 @@ int yrss_debug_partial_merge(yrss_ctx *c, int on)
     if (!c || on < 0 || on > 1)
         return -EINVAL;
     c->dbg.partial_merge = (uint32_t)on;
-    return 0;
-}
-
-int yrss_debug_lookback_polls(yrss_ctx *c, int polls)
-{
-    if (!c || polls < -1 || polls > 1000000)
-        return -EINVAL;
-    c->dbg.lb_polls = polls;
     return 0;
 }
 

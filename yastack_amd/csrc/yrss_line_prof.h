@@ -25,6 +25,13 @@ __device__ uint64_t g_line_prof[2048 * 8 * 8];
         if (t == 0 && blockIdx.x < 2048u)                                              \
             g_line_prof[(blockIdx.x * 8u) * 8u + 7u] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// prologue milestones, slots 1-5 of the unused span-7 row (slot 0 stays 0,
+// so the row never counts as a span)
+#define LPROF_PRO(k)                                                                   \
+    do {                                                                               \
+        if (t == 0 && blockIdx.x < 2048u)                                              \
+            g_line_prof[(blockIdx.x * 8u + 7u) * 8u + (k)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 // the host side (inside the library's extern "C" block): read, then clear (a
 // later batch with fewer workgroups leaves no stale rows)
 #define YRSS_LINE_PROF_HOST_FN                                                         \
@@ -47,6 +54,9 @@ __device__ uint64_t g_line_prof[2048 * 8 * 8];
     } while (0)
 #define LPROF_ENTRY() \
     do {              \
+    } while (0)
+#define LPROF_PRO(k) \
+    do {             \
     } while (0)
 #define YRSS_LINE_PROF_HOST_FN
 #endif
