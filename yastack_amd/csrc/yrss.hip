@@ -915,6 +915,26 @@ __device__ __forceinline__ void list_store1(const ListOut &o, uint32_t d, uint32
         o.p[d] = v;
 }
 
+// The line scatter's lists: always one buffer resource (the host runs it on
+// batches below kLineMaxPkts only, so n x 4 bytes fit the 32-bit record
+// count and offsets), one store form a site: the flat fallback's second
+// store at every site was a pair of branches a quad.
+constexpr uint32_t kLineMaxPkts = 1u << 30;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t line_out(uint32_t *qidx, uint32_t n)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(qidx, 0, (int)(n * 4u), kRsrcWord3);
+}
+template <int kAux>
+__device__ __forceinline__ void line_store4(__amdgpu_buffer_rsrc_t r, uint32_t d, u32x4 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)(d * 4u), 0, kAux);
+}
+template <int kAux>
+__device__ __forceinline__ void line_store1(__amdgpu_buffer_rsrc_t r, uint32_t d, uint32_t v)
+{
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)(d * 4u), 0, kAux);
+}
+
 // ---------------------------------------------------------------------------
 // Kernel 3b: the lists when a parse chunk is longer than the line scatter's
 // span (batches past ~2^29 packets): the stable scatter of packet indices into
@@ -1288,6 +1308,7 @@ struct LineParams {
     uint32_t lmax;             // stage lines: seg / 16 + 2 nb + 1
     uint32_t xcd;              // workgroups of one XCD take consecutive ranges
     uint32_t nt;               // list stores non-temporal only (no sc1): past 64 buckets
+                               // (the instantiation's kNt; the host picks it from this)
     uint32_t early;            // first span's loads before the totals: past 16 buckets
     uint32_t merge;            // partial lines (a range's first / last) as plain stores: L2 merges
     // In-scatter prefixes (fused, up to kFusedMaxNb buckets): no scan kernel
@@ -1372,9 +1393,11 @@ __device__ __forceinline__ void load_groups(const uint16_t *a, uint32_t p0, uint
 // measurement builds (tools/build_ab_lib.sh prof)
 #include "yrss_line_prof.h"
 
-template <bool kPacked, uint32_t kG>
+template <bool kPacked, uint32_t kG, bool kNt>
 __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lines(LineParams P)
 {
+    // list stores: non-temporal only past kListNtBuckets buckets, else nt | sc1
+    constexpr int kNtAux = kNt ? kListAuxMany : kListAux;
     extern __shared__ __attribute__((aligned(16))) uint32_t lsm[];
     const uint32_t nb = P.nb, t = threadIdx.x, lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(t / kWave);
@@ -1430,7 +1453,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // prefixes are loaded beside the first span's streams (one round trip for
     // both) and written once they have arrived
     uint32_t pre0 = 0;
-    const ListOut lout = list_out(P.qidx, P.n);
+    const __amdgpu_buffer_rsrc_t lout = line_out(P.qidx, P.n);
     // The span's streams alternate between two register sets: span g+1's
     // loads issue at the start of span g's phase (b), once its table is in
     // LDS, and are waited for just before span g's copy-out.  vmcnt counts
@@ -1627,21 +1650,21 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         // one non-empty list (all-UDP traffic): 0, 1, ..., n-1, grid-stride
         // 16-byte non-temporal stores (64 MB in 10.7 us,
         // profiles/r02_v8_hbm_write.log)
-        const ListOut lo = list_out(P.qidx, P.n);
+        const __amdgpu_buffer_rsrc_t lo = line_out(P.qidx, P.n);
         const uint32_t ph4 = ph & 3u;
         const uint32_t head = min(P.n, (4u - ph4) & 3u);
         const uint32_t nv = (P.n - head) >> 2;
         const uint32_t T = gridDim.x * blockDim.x;
         const uint32_t id = blockIdx.x * blockDim.x + t;
         if (id < head)
-            list_store1<kListAux>(lo, id, id);
+            line_store1<kListAux>(lo, id, id);
         for (uint32_t v = id; v < nv; v += T) {
             const uint32_t x = head + 4u * v;
-            list_store4<kListAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
+            line_store4<kListAux>(lo, x, u32x4{x, x + 1u, x + 2u, x + 3u});
         }
         const uint32_t e = head + 4u * nv + id;
         if (e < P.n)
-            list_store1<kListAux>(lo, e, e);
+            line_store1<kListAux>(lo, e, e);
         return;
     }
 
@@ -1909,44 +1932,34 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         // (c) copy-out, a quad per thread: whole lines as 16-byte non-temporal
         // stores; the bucket's last line, if the span ends inside it, is
         // carried (unless the range ends here); partial lines word by word
+        // One store site for both line modes, its cache policy a template
+        // argument: the mode, policy and range branches of each quad were a
+        // chain of a dozen scalar and exec branches a turn.
         auto copy_quad = [&](uint32_t v, uint32_t tag, uint32_t gl, const u32x4 &e) {
             const uint32_t mode = tag >> 30;
             const uint32_t a0 = 16u * gl + 4u * (v & 3u);
-            if (mode == 0u) {
-                const uint32_t d = a0 - ph;
-                if (d + 4u <= P.n && d + 4u > d) {
-                    if (P.nt)
-                        list_store4<kListAuxMany>(lout, d, e);
-                    else
-                        list_store4<kListAux>(lout, d, e);
-                    wrote += 4u;
-                    wsum += e.x + e.y + e.z + e.w;
-                } else {
-                    report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
-                }
-            } else if (mode == 2u) {
-                const uint32_t b = tag & 0xffffu, v0 = cs[b], e1 = ve[b];
+            bool go = mode == 0u;
+            if (mode == 2u) {
                 // a partial line (a range's first or last line of a bucket):
-                // its quads inside [v0, e1) still leave as one 16-byte store;
+                // its quads inside [cs, ve) still leave as one 16-byte store;
                 // a quad the bounds cut is left to the cut pass below (word
                 // stores for every quad of such lines tripled the scatter's
                 // store instructions at 256 buckets)
-                if (a0 >= v0 && a0 + 4u <= e1) {
-                    const uint32_t d = a0 - ph;
-                    if (d + 4u <= P.n && d + 4u > d) {
-                        if (P.merge)   // plain: the line's other part meets it in L2
-                            list_store4<0>(lout, d, e);
-                        else if (P.nt)
-                            list_store4<kListAuxMany>(lout, d, e);
-                        else
-                            list_store4<kListAux>(lout, d, e);
-                        wrote += 4u;
-                        wsum += e.x + e.y + e.z + e.w;
-                    } else {
-                        report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
-                    }
-                    return;
-                }
+                const uint32_t b = tag & 0xffffu;
+                go = a0 >= cs[b] && a0 + 4u <= ve[b];
+            }
+            if (!go)
+                return;
+            const uint32_t d = a0 - ph;
+            if (d + 4u <= P.n && d + 4u > d) {
+                if (__builtin_expect(P.merge != 0u, 0) && mode == 2u)
+                    line_store4<0>(lout, d, e);   // plain: the line's other part meets it in L2
+                else
+                    line_store4<kNtAux>(lout, d, e);
+                wrote += 4u;
+                wsum += e.x + e.y + e.z + e.w;
+            } else {
+                report_fault(P.fault, YRSS_FAULT_LIST_RANGE, YRSS_K_SCATTER, g, d);
             }
         };
         // kCopyQ quads a turn, all loaded before any is stored (an
@@ -2000,11 +2013,9 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
                 const uint32_t w = stg[min(so[b] + a, cap)], d = a - ph;
                 if (d < P.n) {
                     if (P.merge)
-                        list_store1<0>(lout, d, w);
-                    else if (P.nt)
-                        list_store1<kListAuxMany>(lout, d, w);
+                        line_store1<0>(lout, d, w);
                     else
-                        list_store1<kListAux>(lout, d, w);
+                        line_store1<kNtAux>(lout, d, w);
                     ++wrote;
                     wsum += w;
                 } else {
@@ -3991,7 +4002,8 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     const LinePlan lp = line_plan(c, lay);
     // the line scatter reads q (when the bucket is not packed with the rank)
     // as 16-byte vectors
-    const bool ranked = compact && lp.ok && (lp.packed || ((uintptr_t)b->q & 15u) == 0);
+    const bool ranked = compact && lp.ok && n < kLineMaxPkts &&
+                        (lp.packed || ((uintptr_t)b->q & 15u) == 0);
     // a line scatter whose per-bucket arrays cannot hold nb is refused before
     // anything is launched (the kernel's own entry check is the backstop)
     if (ranked && !lp.fits && !c->dbg.skip_line_check)
@@ -4016,9 +4028,16 @@ int dispatch_dev_impl(yrss_ctx *c, const struct yrss_dev_batch *b, void *stream)
     uint32_t line_grid = 0, line_lds_bytes = lp.lds, rts = 0, rcs = 0;
     bool fused = false;
     if (ranked) {
+        const bool nt = c->nb > kListNtBuckets;
         line_fn = lp.groups == 4u
-                      ? (lp.packed ? yrss_scatter_lines<true, 4> : yrss_scatter_lines<false, 4>)
-                      : (lp.packed ? yrss_scatter_lines<true, 2> : yrss_scatter_lines<false, 2>);
+                      ? (lp.packed ? (nt ? yrss_scatter_lines<true, 4, true>
+                                         : yrss_scatter_lines<true, 4, false>)
+                                   : (nt ? yrss_scatter_lines<false, 4, true>
+                                         : yrss_scatter_lines<false, 4, false>))
+                      : (lp.packed ? (nt ? yrss_scatter_lines<true, 2, true>
+                                         : yrss_scatter_lines<true, 2, false>)
+                                   : (nt ? yrss_scatter_lines<false, 2, true>
+                                         : yrss_scatter_lines<false, 2, false>));
         // persistent: the resident workgroups, each one contiguous range of
         // spans, never more workgroups than spans
         const uint32_t spans = (uint32_t)(((uint64_t)n + lp.seg - 1) / lp.seg);
