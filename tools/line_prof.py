@@ -23,7 +23,7 @@ import torch  # noqa: E402
 
 from yastack_amd import SoftRss, abi  # noqa: E402
 
-PH = ["a (empty since c61ac37: the table is written in c)", "b tags/carried/place", "wait + wave-0 layout + S2", "c copy-out", "d carry"]
+PH = ["b1 tags/carried (and the next span's loads issued)", "b2 place", "wait + wave-0 layout + S2", "c copy-out", "d carry"]
 
 
 def main() -> int:

@@ -1507,6 +1507,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         // the prefixes first, the streams last: vmcnt counts in issue order,
         // so the prologue can wait for the prefixes alone (the first span's
         // layout and table then overlap its streams' arrival)
+        if (part & 1u) {
         if (wave == 0) {
             // rows past nb read 0 (range check); a span's end past the last
             // chunk is the bucket's total
@@ -1545,9 +1546,12 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             if (k * kLineBlock < ntab)   // (uniform)
                 pt[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo,
                                                              (int)(c0 * 4u + k * step), 0);
-        load_groups(P.rank, p0, pe, tt, pk);
-        if (!kPacked)
-            load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, qk);
+        }
+        if (part & 2u) {
+            load_groups(P.rank, p0, pe, tt, pk);
+            if (!kPacked)
+                load_groups(reinterpret_cast<const uint16_t *>(P.q), p0, pe, tt, qk);
+        }
     };
     // list starts (exclusive scan of totals); workgroup 0 also writes qstart.
     // Every bucket block's total is loaded before the first is scanned: one
@@ -1818,6 +1822,10 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     uint32_t wrote = 0, wsum = 0;
     // the thread's bucket and line slice in the tagging phase
     const uint32_t tk = kLineBlock / nb, tb = t % nb, tj = t / nb;
+    // the small per-bucket loops (carried words, cut quads, carry) start at
+    // the last thread: wave 0 already lays the next span out and holds the
+    // span's critical path
+    const uint32_t tr = kLineBlock - 1u - t;
     auto span = [&](uint32_t g, uint32_t s, const u32x4 (&pk)[kG], const u32x4 (&qk)[kG],
                     u32x4 (&pkn)[kG], u32x4 (&qkn)[kG]) {
         const uint32_t p0 = g * P.seg, len = span_end(g) - p0;
@@ -1828,7 +1836,6 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         LPROF(0);
         // (the table was written in the previous span's copy-out, or the
         // prologue: two barriers a span)
-        LPROF(1);
         const uint32_t L = __builtin_amdgcn_readfirstlane(misc[4u + s]);
         // (b) three independent writes into LDS, no barrier between them:
         // - each stage line tagged with its bucket, list line and copy mode
@@ -1857,7 +1864,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         // the carried words, a quad a thread (a 16-byte copy where the quad
         // is whole and its stage slots aligned, else word by word: a whole-quad
         // write past ce would race the placement of the span's own packets)
-        for (uint32_t e = t; e < 4u * nb; e += kLineBlock) {
+        for (uint32_t e = tr; e < 4u * nb; e += kLineBlock) {
             const uint32_t b = e >> 2, q4 = 4u * (e & 3u);
             const uint32_t n = ce[b] - cs[b], base = so[b] + cs[b];
             if (q4 >= n)
@@ -1874,6 +1881,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         }
         // (a packed bucket past nb reads some other LDS word as its slot
         // base: the slot is clamped and the hole it leaves is reported)
+        LPROF(1);   // (tags and carried words issued; the placement next)
         auto place = [&](auto ragged) {
             // every slot base of the thread's packets is read before any
             // stage write: a read after a write to the same LDS is ordered
@@ -1999,7 +2007,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         // while some bucket's first valid position is off a quad: layout
         // records that, so a middle span usually skips the pass)
         const uint32_t ncut = last || misc[6u + s] ? 8u * nb : 0u;
-        for (uint32_t e = t; e < ncut; e += kLineBlock) {
+        for (uint32_t e = tr; e < ncut; e += kLineBlock) {
             const uint32_t b = e >> 3, k = (e >> 2) & 1u, j = e & 3u;
             const uint32_t v0 = cs[b], e1 = ve[b];
             const uint32_t qb = (k ? e1 : v0) & ~3u, a = qb + j;
@@ -2029,7 +2037,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             // a quad a thread: a 16-byte copy where the stage slots are
             // aligned (the words past the end carry nothing the next span
             // reads), else word by word
-            for (uint32_t e = t; e < 4u * nb; e += kLineBlock) {
+            for (uint32_t e = tr; e < 4u * nb; e += kLineBlock) {
                 const uint32_t b = e >> 2, q4 = 4u * (e & 3u);
                 const uint32_t e1 = ve[b], nv = max(cs[b], e1 & ~15u);
                 const uint32_t n = e1 - nv, base = so[b] + nv;
