@@ -34,6 +34,7 @@ def main() -> int:
     ap.add_argument("--groups", type=int, default=0,
                     help="force the line-scatter kernel (yrss_debug_line_groups: 2 / 4 kG); "
                          "needs a -DYRSS_TEST_HOOKS build")
+    ap.add_argument("--profile", default="tcp4", choices=("tcp4", "imix", "udp4"))
     ap.add_argument("--scan-kernel", type=int, default=0,
                     help="1: list prefixes from the scan kernel (yrss_tuning.scan_kernel)")
     args = ap.parse_args()
@@ -47,7 +48,8 @@ def main() -> int:
             assert e._lib.yrss_debug_line_groups(e._ctx, args.groups, 0) == 0
         if args.scan_kernel:
             e.set_tuning(scan_kernel=1)
-        w, l = e.synth(abi.SYN_TCP4, n, 0)
+        w, l = e.synth({"tcp4": abi.SYN_TCP4, "imix": abi.SYN_IMIX, "udp4": abi.SYN_UDP4}[args.profile],
+                       n, 0)
         out = e.alloc_out(n, w.device)
         buf = np.zeros(2048 * 8 * 8, np.uint64)
         for _ in range(4):
@@ -67,7 +69,7 @@ def main() -> int:
             print(f"q{npr}: no spans (one-list batch)")
             e.close()
             continue
-        print(f"q{npr} groups {args.groups} scan_kernel {args.scan_kernel}: {blocks} workgroups, spans per workgroup {spans.min()}-{spans.max()}")
+        print(f"q{npr} {args.profile} groups {args.groups} scan_kernel {args.scan_kernel}: {blocks} workgroups, spans per workgroup {spans.min()}-{spans.max()}")
         for k, name in enumerate(PH):
             v = d[:, :, k][m[:, :, k]]
             if v.size == 0:

@@ -1288,6 +1288,9 @@ constexpr uint32_t line_nb_max(uint32_t g) { return 64u * line_bucket_regs(g); }
 // each (up to kFusedRows): its counts over the range's chunks and its bins of
 // the earlier ranges; the range bins are [nb][kLbMaxWgs].
 constexpr uint32_t kFusedMaxNb = 16;
+// the bucket-major tagging is kept while no thread gets more than kTagIters
+// of a bucket's lines
+constexpr uint32_t kTagIters = 6;
 constexpr uint32_t kFusedRows = 3;          // bucket rows a loading wave (waves 1-7)
 constexpr uint32_t kFusedMaxCols = 256;      // chunks a range: 4 a lane
 constexpr uint32_t kFusedMaxRanges = 512;    // earlier ranges' bins: 8 a lane
@@ -1348,7 +1351,7 @@ __host__ __device__ inline LineLds line_lds(uint32_t nb, uint32_t gshift, uint32
     L.so = take(2u * nb);    // stage index = so[b] + adjusted position
     L.rb = take(2u * nb);    // prefix table row bias (to stage slots)
     L.lsl = take(2u * (nb + 1u));   // first stage line of each bucket
-    L.misc = take(8);
+    L.misc = take(10);   // [8 + s]: the tagging's form for layout set s
     L.tab = take(nb * ((1u << gshift) + 1u));   // rows of 2^gshift + 1 words (odd: banks)
     L.cb = take(16u * nb);
     L.ltag = take(lmax);  // bucket | copy mode << 30 per stage line
@@ -1404,7 +1407,8 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // Capacity, checked before any barrier (the condition is uniform): a
     // plan past what this instantiation holds reports and leaves, instead of
     // running on unwritten per-bucket words (see line_nb_max)
-    if (nb > line_nb_max(kG) || (nb << P.gshift) > line_tab_max(kG)) {
+    if (nb > line_nb_max(kG) || (nb << P.gshift) > line_tab_max(kG) ||
+        P.lmax > kLineBlock * (kG == 4u ? 5u : 2u)) {
         if (t == 0)
             report_fault(P.fault, YRSS_FAULT_LINE_CAPACITY, YRSS_K_SCATTER, nb, line_nb_max(kG));
         return;
@@ -1751,7 +1755,7 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         const uint32_t *pcs = cs + (s ^ 1u) * nb, *pve = ve + (s ^ 1u) * nb;
         uint32_t *wcs = cs + s * nb, *wve = ve + s * nb, *wce = ce + s * nb, *wso = so + s * nb;
         uint32_t *wrb = rb + s * nb, *wlsl = lsl + s * (nb + 1u);
-        uint32_t lines = 0;
+        uint32_t lines = 0, mx = 0;   // mx: a bucket's most stage lines
         bool cut = false;   // a bucket's first valid position not on a quad: cut quads
         // (lane hidden from the optimiser: the per-lane LDS addresses of
         // both sets were hoisted out of the span loop and spilled)
@@ -1780,6 +1784,16 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             }
             lines += __shfl(x, kWave - 1, kWave);
             cut |= __ballot(b < nb && (v0 & 3u) != 0u) != 0ull;
+            mx = max(mx, nl);
+        }
+        if (kG == 4u) {   // (the skewed form is built past 128 buckets only: in
+                          // the kG = 2 kernel its code cost 0.6-1 us a batch at
+                          // 4-9 buckets, profiles/r06_ab_c11_*, r06_ab_c12_*)
+#pragma unroll
+            for (uint32_t d = 1; d < (uint32_t)kWave; d <<= 1)
+                mx = max(mx, (uint32_t)__shfl_xor(mx, d, kWave));
+        } else {
+            mx = 0u;
         }
         if (lane == 0) {
             if (lines > P.lmax) {
@@ -1789,6 +1803,9 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
             wlsl[nb] = lines;
             misc[4u + s] = lines;
             misc[6u + s] = cut ? 1u : 0u;
+            // a thread to a bucket's lines unless that leaves some thread more
+            // than kTagIters of them (one bucket holding most of the traffic)
+            misc[8u + s] = mx > kTagIters * (kLineBlock / nb) ? 1u : 0u;
         }
     };
     // span g's prefix table, tab[b][c] = prefix at chunk c + rb[b] (rows of
@@ -1820,8 +1837,13 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
     // its packets once, so the sum must be that of its packet indices (two
     // packets on one slot leave another slot with an earlier span's index)
     uint32_t wrote = 0, wsum = 0;
-    // the thread's bucket and line slice in the tagging phase
+    // the tagging: a thread to a bucket's lines (bucket tb, lines tj + k tk),
+    // or, on skewed spans, a thread to lines t + 512 k with the binary
+    // search's first step tag_hi (the highest power of two below nb);
+    // lmax <= 512 kTagLines
     const uint32_t tk = kLineBlock / nb, tb = t % nb, tj = t / nb;
+    const uint32_t tag_hi = nb > 1u ? 1u << (31u - __builtin_clz(nb - 1u)) : 0u;
+    constexpr uint32_t kTagLines = kG == 4u ? 5u : 2u;
     // the small per-bucket loops (carried words, cut quads, carry) start at
     // the last thread: wave 0 already lays the next span out and holds the
     // span's critical path
@@ -1848,17 +1870,63 @@ __global__ __launch_bounds__(kLineBlock, kG == 4u ? 2 : 4) void yrss_scatter_lin
         // - every packet at slot = tab[b][chunk] + rank.
         if (!last)
             load_span(g + 1u, pkn, qkn);
-        if (tj < tk) {
+        if (kG != 4u || !misc[8u + s]) {
+            // a thread to a bucket's lines: lines tj, tj + tk, ... of bucket tb
+            // (tk = 512 / nb threads to a bucket), one read of the bucket's
+            // bounds, then stores
             const uint32_t b = opaque(tb);   // (addresses not hoisted: registers)
-            // (bounded by the span's line count whatever the words say)
-            const uint32_t l0 = lsl[b], l1 = L ? min(lsl[b + 1u], L) : 0u, v0 = cs[b], e1 = ve[b];
-            for (uint32_t l = l0 + tj; l < l1; l += tk) {
-                const uint32_t gl = l - l0 + (v0 >> 4);
-                const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
-                                      : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
-                                                                                      : 2u;
-                ltag[l] = b | mode << 30;
-                lgl[l] = gl;
+            if (tj < tk) {
+                // (bounded by the span's line count whatever the words say)
+                const uint32_t l0 = lsl[b], l1 = L ? min(lsl[b + 1u], L) : 0u, v0 = cs[b],
+                               e1 = ve[b];
+                for (uint32_t l = l0 + tj; l < l1; l += tk) {
+                    const uint32_t gl = l - l0 + (v0 >> 4);
+                    const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
+                                          : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
+                                                                                          : 2u;
+                    ltag[l] = b | mode << 30;
+                    lgl[l] = gl;
+                }
+            }
+        } else {
+            // skewed buckets (layout's misc[8 + s]): a thread to each of stage
+            // lines t, t + 512, ... (< L), its
+            // bucket found by a binary search over the buckets' first lines,
+            // the searches of a thread's lines interleaved (their LDS reads
+            // independent): balanced whatever the buckets' sizes.  A thread
+            // to a bucket's lines (512 / nb threads a bucket) left one bucket
+            // holding most of the traffic to a few threads: IMIX at 256
+            // buckets, every UDP packet in queue 2, spent 22.7 us a span
+            // tagging against 3.2 for all-TCP (profiles/r06_lineprof_skew_*);
+            // on balanced buckets the search's log2 nb LDS round trips cost
+            // more than the bucket-major loop (all-TCP at 256 buckets: scatter
+            // 50 -> 58 us, profiles/r06_ab_c10_*), hence the choice a span
+            uint32_t lb[kTagLines];
+#pragma unroll
+            for (uint32_t i = 0; i < kTagLines; ++i)
+                lb[i] = 0u;
+            for (uint32_t st = tag_hi; st; st >>= 1) {
+#pragma unroll
+                for (uint32_t i = 0; i < kTagLines; ++i) {
+                    const uint32_t l = t + i * kLineBlock, c = lb[i] + st;
+                    if (c < nb && lsl[c] <= l)
+                        lb[i] = c;
+                }
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < kTagLines; ++i) {
+                const uint32_t l = t + i * kLineBlock;
+                // (bounded by the span's line count whatever the words say)
+                if (l < L) {
+                    const uint32_t b = lb[i];
+                    const uint32_t l0 = lsl[b], v0 = cs[b], e1 = ve[b];
+                    const uint32_t gl = l - l0 + (v0 >> 4);
+                    const uint32_t mode = 16u * gl >= v0 && 16u * gl + 16u <= e1 ? 0u
+                                          : !last && gl == (e1 >> 4) && (e1 & 15u) != 0u ? 1u
+                                                                                          : 2u;
+                    ltag[l] = b | mode << 30;
+                    lgl[l] = gl;
+                }
             }
         }
         // the carried words, a quad a thread (a 16-byte copy where the quad
@@ -3185,6 +3253,8 @@ LinePlan line_plan(const yrss_ctx *c, const Layout &lay)
         return p;
     p.seg = lay.chunk << p.gshift;
     p.lmax = p.seg / 16u + 2u * nb + 1u;   // a bucket's lines <= (its packets + 30) / 16
+    // the tagging's lines a thread (kTagLines) must reach every stage line
+    p.fits = p.fits && p.lmax <= (uint32_t)kLineBlock * (p.groups == 4u ? 5u : 2u);
     p.lds = line_lds(nb, p.gshift, p.lmax).words * 4u;
     if (p.lds > 160u * 1024u)
         return p;
