@@ -26,7 +26,8 @@ import torch  # noqa: E402
 
 from yastack_amd import SoftRss, abi  # noqa: E402
 
-PROFILES = {"udp4": abi.SYN_UDP4, "tcp4": abi.SYN_TCP4, "imix": abi.SYN_IMIX}
+PROFILES = {"udp4": abi.SYN_UDP4, "tcp4": abi.SYN_TCP4, "imix": abi.SYN_IMIX,
+            "jumbo_tcp4": abi.SYN_JUMBO_TCP4}
 
 
 def main() -> int:

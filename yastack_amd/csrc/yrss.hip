@@ -474,9 +474,14 @@ __device__ __forceinline__ void process_tile(const ParseParams &P, const uint32_
                 trunc = true;
             }
         }
-        // hash % d exactly (Lemire fastmod, 64-bit M), then +q_off (:2031-2034)
-        const uint64_t low = P.mod_m * (uint64_t)h;
-        const uint32_t rem = (uint32_t)__umul64hi(low, (uint64_t)P.mod_d);
+        // hash % d exactly, then +q_off (:2031-2034): a mask when d is a power
+        // of two (d = 2 at the reference's nb_procs 3 with dispatch_only_core;
+        // the branch is uniform), else Lemire's fastmod with a 64-bit M.  The
+        // mask saved the hashed parse kernel 1.3-2.9 us in four same-process
+        // A/Bs (profiles/r06_parse_abl_*, r06_ab_c16_*)
+        const uint32_t rem = (P.mod_d & (P.mod_d - 1u)) == 0u
+                                 ? h & (P.mod_d - 1u)
+                                 : (uint32_t)__umul64hi(P.mod_m * (uint64_t)h, (uint64_t)P.mod_d);
         qv = (int)(uint16_t)(rem + P.q_off);
         if (trunc) {
             qv = YRSS_Q_TRUNCATED;
