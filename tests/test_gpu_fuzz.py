@@ -52,6 +52,34 @@ def test_random_configs(dev, oracle_mod, case):
         run_and_compare(eng, oracle_mod, (npr, nq, soft, only), profile, n, stride, first=first)
 
 
+def _large_cases(count, seed):
+    # batches of many spans and many scatter ranges (the line scatter's
+    # in-scatter prefixes up to 16 buckets, the scan kernel past them), with
+    # the prefix form, the XCD mapping and the parse grid drawn as well
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < count:
+        npr = int(rng.choice([2, 3, 4, 8, 16, 64, 255]))
+        nq = int(rng.choice([1, 2, 3, 4, 7, 15, 16, 17, 64]))
+        only = int(rng.integers(0, 2))
+        profile = int(rng.choice([1, 2, 4, 5, 6]))
+        n = int(rng.integers(1 << 17, 1 << 21))
+        first = int(rng.integers(0, 1 << 40))
+        tune = (int(rng.integers(0, 2)), int(rng.choice([-1, 0, 1])),
+                int(rng.choice([0, 64, 256])))
+        out.append((npr, nq, only, profile, n, first, tune))
+    return out
+
+
+@pytest.mark.parametrize("case", _large_cases(int(os.environ.get("YRSS_FUZZ_LARGE_CASES", "6")),
+                                              int(os.environ.get("YRSS_FUZZ_SEED", "2024"))))
+def test_random_large_batches(dev, oracle_mod, case):
+    npr, nq, only, profile, n, first, (scan_kernel, xcd, blocks) = case
+    with SoftRss(npr, nq, 1, only, device=0, max_burst=0) as eng:
+        eng.set_tuning(scan_kernel=scan_kernel, scatter_xcd=xcd, parse_blocks=blocks)
+        run_and_compare(eng, oracle_mod, (npr, nq, 1, only), profile, n, 64, first=first)
+
+
 def test_two_threads_two_contexts(dev, oracle_mod):
     cfgs = [(3, 3, 1, 1), (8, 6, 1, 0)]
     frames = _frames(oracle_mod, 6000, 77)
