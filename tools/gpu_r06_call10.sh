@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the ablib/ libraries: python tools/build_measure_libs.py)
 # round-6 call: where the hashed parse kernel's extra time goes (measurement
 # builds, lists wrong by design where they drop work):
 #   ablib/libyrss_pA.so  no counting and no ranks in the parse kernel

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the ablib/ libraries: python tools/build_measure_libs.py)
 # round-6 call: the parse kernel with counts but no ranks (ablib/libyrss_pD.so,
 # kCount 1's work in the kCount 2 kernel; lists wrong) and with no counting at
 # all (ablib/libyrss_pA.so), against the tree, 12 rounds, hashed traffic

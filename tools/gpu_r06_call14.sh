@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the ablib/ libraries: python tools/build_measure_libs.py)
 # round-6 call: the parse kernel with two tiles of loads ahead (three register
 # sets, ablib/libyrss_pf2.so): parity through that library, then a 12-round
 # same-process A/B against the tree on hashed and UDP traffic

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the ablib/ libraries: python tools/build_measure_libs.py)
 # Round-6 measurements: upper bounds, from measurement-only builds of the tree
 # (lists wrong by design, their end-of-range check taken out):
 #   ablib/libyrss_noload.so  span g+1's rank-stream loads replaced by span g's
