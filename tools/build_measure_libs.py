@@ -18,6 +18,7 @@ section 14):
   pC      hash % d as h & (d - 1) (exact for d a power of two)
   pD      the parse kernel with counts but no ranks
   pf2     two tiles of loads ahead in the parse kernel (three register sets)
+  grid1   the line scatter at one workgroup a CU (twice the spans a workgroup)
 
 Lists are wrong by design in noload, noconf, pA and pD; their end-of-range
 check is removed so a faulting batch does not time the fault path.
@@ -106,6 +107,13 @@ VARIANTS = {
         } else if (kCount == 5) {
             uint32_t before = 0;"""),
         NO_RANGE_CHECK,
+    ],
+    "grid1": [
+        ("""        line_grid = std::max(1u, std::min(spans, resident_blocks(c, (const void *)line_fn,
+                                                                 kLineBlock, lp.lds)));""",
+         """        line_grid = std::max(1u, std::min(spans, resident_blocks(c, (const void *)line_fn,
+                                                                 kLineBlock, lp.lds)));
+        line_grid = std::min(line_grid, (uint32_t)c->cus);   // MEASUREMENT: one workgroup a CU"""),
     ],
     "pf2": [
         ("""    uint32_t tA = 0, sA = 0, tB = 0, sB = 0;
