@@ -80,10 +80,11 @@ def parse_args(argv=None):
     ap.add_argument("--tune", default="",
                     help="layout overrides for measurements, k=v[,k=v] (yrss_set_tuning "
                          "fields: chunk_tiles, span_tiles, parse_blocks, scatter_xcd, scan_kernel)")
-    ap.add_argument("--extra-configs", default="vlan6_tcp,jumbo_tcp4",
+    ap.add_argument("--extra-configs", default="imix,vlan6_tcp,jumbo_tcp4",
                     help="after the headline, each rank also classifies a --pkts shard of "
-                         "these profiles (BASELINE configs[3], configs[4]: the 8-GPU "
-                         "configs), reported under configs_extra, never as value ('' = off)")
+                         "these profiles (BASELINE configs[2] IMIX, configs[3] and configs[4], "
+                         "the 8-GPU configs), reported under configs_extra, never as value "
+                         "('' = off)")
     ap.add_argument("--test-hooks", default="",
                     help="measurements only: run libyrss_test.so with its yrss_debug_* hooks, "
                          "k=v[,k=v] (merge, groups); the line says so")
@@ -794,7 +795,8 @@ def run_extra_config(eng, profile, args, world, rank, devices):
     """One more BASELINE config after the headline: each rank classifies its own
     --pkts shard of `profile` (weak scaling, no collective on the data path),
     timed like the headline (barrier + synchronize on both sides, max over
-    ranks) over min(steps, 20) steps of two rotated batches; the parse kernel
+    ranks) over min(steps, 50) steps of four rotated batches after min(warmup,
+    20) untimed ones, as the headline rotates its batches; the parse kernel
     timed by events on its own dispatch packet; then checked against the oracle
     (q and hash of the first --check packets, the whole per-queue lists)."""
     import numpy as np
@@ -805,22 +807,23 @@ def run_extra_config(eng, profile, args, world, rank, devices):
 
     n = args.pkts
     nbq = args.nb_queues or args.nb_procs
+    nbat = 4
     bats = []
-    for k in range(2):
-        w_k, l_k = eng.synth(PROFILES[profile], n, (rank * 2 + k) * n, SEED, NFLOWS[profile],
+    for k in range(nbat):
+        w_k, l_k = eng.synth(PROFILES[profile], n, (rank * nbat + k) * n, SEED, NFLOWS[profile],
                              args.stride)
         bats.append((w_k, l_k, eng.alloc_out(n, w_k.device)))
     it = [0]
 
     def step():
-        w_k, l_k, o_k = bats[it[0] % 2]
+        w_k, l_k, o_k = bats[it[0] % nbat]
         it[0] += 1
         eng.dispatch_dev(w_k, l_k, args.stride, n, out=o_k)
 
-    for _ in range(5):
+    for _ in range(max(5, min(args.warmup, 20))):
         step()
     torch.cuda.synchronize()
-    steps = max(1, min(args.steps, 20))
+    steps = max(1, min(args.steps, 50))
     eng.timing_enable(1 << abi.K_PARSE_HASH)
     barrier(world)
     torch.cuda.synchronize()
@@ -835,7 +838,7 @@ def run_extra_config(eng, profile, args, world, rank, devices):
     eng.timing_enable(0)
     k_s = max_over_ranks(k_ms / max(k_cnt, 1) / 1e3, world)
     # the check, on the batch the last step classified
-    w_k, l_k, o_k = bats[(it[0] - 1) % 2]
+    w_k, l_k, o_k = bats[(it[0] - 1) % nbat]
     m = min(args.check or (1 << 20), n)
     c = oracle.cfg(args.nb_procs, nbq, 1, args.dispatch_only_core)
     q_ref, h_ref = oracle.dispatch_windows(w_k[: m * args.stride].cpu().numpy(), args.stride,
@@ -856,6 +859,7 @@ def run_extra_config(eng, profile, args, world, rank, devices):
             "value": round(total / elapsed / 1e6, 2), "unit": "Mpkt/s",
             "ms_per_step": round(elapsed / steps * 1e3, 4),
             "parse_us": round(k_s * 1e6, 2),
+            "outside_parse_us": round(elapsed / steps * 1e6 - k_s * 1e6, 2) if k_s else None,
             "roofline_frac": round(bpp * n / k_s / 1e9 / HBM_PEAK_GBS, 4) if k_s else None,
             "ranks_checked": chk["ranks_checked"], "bit_exact": chk["bit_exact"],
             "pkts_checked": chk["pkts_checked"]}
