@@ -228,13 +228,17 @@ def test_burst_api_mbufs(dev, oracle_mod):
             assert rss == want[i][1]
 
 
-@pytest.mark.parametrize("profile", [abi.SYN_UDP4, abi.SYN_TCP4, abi.SYN_IMIX, abi.SYN_FUZZ])
-def test_full_size_bit_exact(dev, oracle_mod, profile):
-    """BASELINE size (2^24 packets/GPU) compared packet-for-packet."""
+@pytest.mark.parametrize("profile,nflows", [(abi.SYN_UDP4, 1 << 20), (abi.SYN_TCP4, 1 << 20),
+                                            (abi.SYN_IMIX, 1 << 20), (abi.SYN_FUZZ, 1 << 20),
+                                            (abi.SYN_VLAN6_TCP, 1 << 22),
+                                            (abi.SYN_JUMBO_TCP4, 1 << 24)])
+def test_full_size_bit_exact(dev, oracle_mod, profile, nflows):
+    """BASELINE size (2^24 packets/GPU) compared packet-for-packet, configs[3] and
+    configs[4] with their own flow counts (4M, 16M)."""
     n = 1 << 24
     with SoftRss(3, 3, 1, 1, device=0, max_burst=0) as eng:
         stride = 64
-        win, lens = eng.synth(profile, n, 0, stride=stride)
+        win, lens = eng.synth(profile, n, 0, nflows=nflows, stride=stride)
         res = eng.dispatch_dev(win, lens, stride, n)
         torch.cuda.synchronize()
         c = oracle_mod.cfg(3, 3, 1, 1)
